@@ -1,0 +1,135 @@
+/*
+ * psgd.h — C ABI of the MI355X-native PowerSGD codec (libpsgd.so).
+ *
+ * Drop-in boundary for the hot path of epfml/powersgd. Every entry point names the
+ * reference interface it replaces (paths relative to the reference repository):
+ *
+ *   psgd_should_compress   powersgd/powersgd.py:101-105 (+ avg_compressed_size :292-294)
+ *   psgd_plan_create       BasicPowerSGD.__init__       powersgd/powersgd.py:114-144, :253-263
+ *   psgd_plan_* queries    _ps_buffer/_qs_buffer layout :130-144, compression_rate :265-275
+ *   psgd_compress          one power iteration          powersgd/powersgd.py:172-202
+ *                          (orthogonalize :188 -> orthogonalization.py:4-8; bmm :189-193;
+ *                           local error-feedback update :195-202)
+ *   psgd_decompress        approximation + un-batching  powersgd/powersgd.py:211-230
+ *   psgd_aggregate         BasicPowerSGD.aggregate      powersgd/powersgd.py:146-235 (world size 1)
+ *   psgd_flat_*            AllReduce.aggregate          powersgd/powersgd.py:22-31,
+ *                          pack / allreduce_average      powersgd/utils.py:6-10, :43-49
+ *
+ * Conventions
+ *  - No torch types. Device buffers are plain pointers on the plan's device; `stream` is a
+ *    hipStream_t passed as void*. All compute calls are stream-ordered and asynchronous, do no
+ *    device allocation and no host synchronisation (except a one-off pointer-table upload when
+ *    the set of gradient pointers changes).
+ *  - Ownership: the caller owns gradients, outputs, the P/Q state buffers and the workspace;
+ *    the plan owns host-side layout only.
+ *  - Gradients are mutated in place into the error-feedback residual (reference :230).
+ *  - P/Q factors are always fp32 (reference :241-251 allocates them in the default dtype).
+ *  - Errors: every call returns a psgd_status; psgd_last_error() returns a thread-local message.
+ *    PSGD_ERR_INDEX mirrors the reference's IndexError (no tensors, :118), PSGD_ERR_DTYPE its
+ *    RuntimeError on unsupported dtypes (:189), PSGD_ERR_LAYOUT its RuntimeError on
+ *    non-viewable tensors (:289).
+ *  - Not re-entrant per plan; one plan per device/process (reference: single-threaded, :146).
+ */
+#ifndef PSGD_H
+#define PSGD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct psgd_plan psgd_plan;
+typedef struct psgd_flat psgd_flat;
+
+enum psgd_status {
+    PSGD_OK = 0,
+    PSGD_ERR_INDEX = 1,   /* empty tensor list (reference IndexError)              */
+    PSGD_ERR_VALUE = 2,   /* invalid argument (rank < 1, iterations out of range…) */
+    PSGD_ERR_DTYPE = 3,   /* unsupported dtype                                      */
+    PSGD_ERR_LAYOUT = 4,  /* unsupported layout / empty tensor                      */
+    PSGD_ERR_DEVICE = 5,  /* HIP runtime error                                      */
+    PSGD_ERR_STATE = 6    /* call order error (e.g. compute before psgd_plan_bind)  */
+};
+
+enum psgd_dtype { PSGD_F32 = 0, PSGD_BF16 = 1 };
+
+/* Largest num_iters_per_step a plan accepts. */
+#define PSGD_MAX_ITERS 16
+
+int psgd_version(void);
+const char* psgd_last_error(void);
+
+/* Compression policy: numel / (0.5*iters*min(rank,min(shape))*sum(shape)) > min_rate,
+ * evaluated on the ORIGINAL tensor shape (reference powersgd.py:101-105, :292-294). */
+int psgd_should_compress(const int64_t* shape, int32_t ndim, int32_t rank,
+                         int32_t num_iters_per_step, double min_compression_rate,
+                         int32_t* out_flag);
+
+/* ---------------------------------------------------------------- codec plan ------ */
+/* `dims` holds the concatenated shapes of the `num_tensors` compressed tensors
+ * (ndims[i] entries each). Matrices are the view [shape[0], numel/shape[0]]; they are
+ * grouped by matrix shape in first-appearance order, and the P (resp. Q) state buffer
+ * is the concatenation over groups of [count, n, r] (resp. [count, m, r]) fp32 arrays,
+ * r = min(rank, n, m) — byte-for-byte the reference's _ps_buffer/_qs_buffer layout. */
+int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tensors,
+                     int32_t rank, int32_t num_iters_per_step, int32_t dtype,
+                     psgd_plan** out_plan);
+int psgd_plan_destroy(psgd_plan* plan);
+
+int psgd_plan_num_groups(const psgd_plan* plan, int32_t* out);
+int psgd_plan_group(const psgd_plan* plan, int32_t g, int64_t* n, int64_t* m, int32_t* r,
+                    int32_t* count);
+int psgd_plan_factor_numel(const psgd_plan* plan, int64_t* p_numel, int64_t* q_numel);
+/* Element offset of compressed tensor i inside the flat output buffer, and the total
+ * number of elements that buffer needs. The layout is dense in tensor order (torch.cat). */
+int psgd_plan_output_offset(const psgd_plan* plan, int32_t i, int64_t* offset);
+int psgd_plan_output_numel(const psgd_plan* plan, int64_t* numel);
+int psgd_plan_workspace_bytes(const psgd_plan* plan, int64_t* bytes);
+/* reference compression_rate / uncompressed_num_floats / compressed_num_floats (:265-275) */
+int psgd_plan_compression_rate(const psgd_plan* plan, double* rate, double* uncompressed,
+                               double* compressed);
+
+/* Bind caller-owned device memory: P state [p_numel] fp32, Q state [q_numel] fp32 and a
+ * workspace of psgd_plan_workspace_bytes() bytes (16-byte aligned). Uploads the static
+ * layout tables (synchronous; call once). */
+int psgd_plan_bind(psgd_plan* plan, int32_t device, float* p_state, float* q_state,
+                   void* workspace);
+
+/* Which state buffer iteration `it` of step `step` produces (and the caller must SUM-
+ * all-reduce before the next call when world size > 1): 0 = Q (even), 1 = P (odd).
+ * Parity = (step*num_iters_per_step + it) % 2 (reference :174). */
+int psgd_out_factor(const psgd_plan* plan, int64_t step, int32_t it, int32_t* which);
+
+/* One power iteration on every compressed matrix: orthonormalise the in-factor (rank 1:
+ * one joint norm per shape group; rank > 1: Householder QR per matrix), then the
+ * tall-skinny product with the error-feedback matrix G_it = G_0 - sum_{j<it} P_j Q_j^T
+ * (formed on the fly, gradients are not written). Leaves the LOCAL factor in the out-
+ * factor state buffer. `grads[i]` = device pointer of compressed tensor i (contiguous). */
+int psgd_compress(psgd_plan* plan, void* const* grads, int64_t step, int32_t it, void* stream);
+
+/* Fused final pass: grads[i] <- G_0 - sum_k P_k Q_k^T (local factors) and
+ * out[i] <- (1/world_size) * sum_k P_k Qbar_k^T (all-reduced factors); `out` is the flat
+ * output buffer (psgd_plan_output_offset). Call after the last psgd_compress (and its
+ * all-reduce). */
+int psgd_decompress(psgd_plan* plan, void* const* grads, void* out, int64_t step,
+                    int32_t world_size, void* stream);
+
+/* Whole BasicPowerSGD.aggregate step for world size 1. */
+int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);
+
+/* ------------------------------------------ uncompressed tensors: flat average ------ */
+/* AllReduce.aggregate minus the collective: flat[off_i + e] = x_i[e] / world_size (exact
+ * copy when world_size == 1), then x_i[e] = 0. The caller SUM-all-reduces `flat` and
+ * returns views of it (reference powersgd.py:22-31). Offsets are dense (torch.cat). */
+int psgd_flat_create(const int64_t* numels, int32_t count, int32_t dtype, psgd_flat** out);
+int psgd_flat_destroy(psgd_flat* flat);
+int psgd_flat_workspace_bytes(const psgd_flat* flat, int64_t* bytes);
+int psgd_flat_bind(psgd_flat* flat, int32_t device, void* workspace);
+int psgd_flat_pack(psgd_flat* flat, void* const* tensors, void* flat_out, int32_t world_size,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSGD_H */

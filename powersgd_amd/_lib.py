@@ -1,0 +1,201 @@
+"""ctypes binding of libpsgd.so (the C ABI in include/psgd.h).
+
+The library is built in-tree (powersgd_amd/_lib/libpsgd.so, see powersgd_amd/csrc/Makefile).
+There is no fallback: if the library is missing, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libpsgd.so")
+
+PSGD_F32, PSGD_BF16 = 0, 1
+_STATUS_NAMES = {1: "INDEX", 2: "VALUE", 3: "DTYPE", 4: "LAYOUT", 5: "DEVICE", 6: "STATE"}
+
+_i32, _i64, _dbl, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+_P_i64, _P_i32, _P_dbl = ctypes.POINTER(_i64), ctypes.POINTER(_i32), ctypes.POINTER(_dbl)
+
+_SIGNATURES = {
+    "psgd_version": ([], _i32),
+    "psgd_last_error": ([], ctypes.c_char_p),
+    "psgd_should_compress": ([_P_i64, _i32, _i32, _i32, _dbl, _P_i32], _i32),
+    "psgd_plan_create": ([_P_i64, _P_i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_vp)], _i32),
+    "psgd_plan_destroy": ([_vp], _i32),
+    "psgd_plan_num_groups": ([_vp, _P_i32], _i32),
+    "psgd_plan_group": ([_vp, _i32, _P_i64, _P_i64, _P_i32, _P_i32], _i32),
+    "psgd_plan_factor_numel": ([_vp, _P_i64, _P_i64], _i32),
+    "psgd_plan_output_offset": ([_vp, _i32, _P_i64], _i32),
+    "psgd_plan_output_numel": ([_vp, _P_i64], _i32),
+    "psgd_plan_workspace_bytes": ([_vp, _P_i64], _i32),
+    "psgd_plan_compression_rate": ([_vp, _P_dbl, _P_dbl, _P_dbl], _i32),
+    "psgd_plan_bind": ([_vp, _i32, _vp, _vp, _vp], _i32),
+    "psgd_out_factor": ([_vp, _i64, _i32, _P_i32], _i32),
+    "psgd_compress": ([_vp, _vp, _i64, _i32, _vp], _i32),
+    "psgd_decompress": ([_vp, _vp, _vp, _i64, _i32, _vp], _i32),
+    "psgd_aggregate": ([_vp, _vp, _vp, _i64, _vp], _i32),
+    "psgd_flat_create": ([_P_i64, _i32, _i32, ctypes.POINTER(_vp)], _i32),
+    "psgd_flat_destroy": ([_vp], _i32),
+    "psgd_flat_workspace_bytes": ([_vp, _P_i64], _i32),
+    "psgd_flat_bind": ([_vp, _i32, _vp], _i32),
+    "psgd_flat_pack": ([_vp, _vp, _vp, _i32, _vp], _i32),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpsgd.so once; raise loudly when it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C powersgd_amd/csrc`. powersgd_amd has no CPU fallback."
+            )
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = handle
+    return _lib
+
+
+def check(status: int) -> None:
+    if status == 0:
+        return
+    msg = lib().psgd_last_error().decode(errors="replace")
+    name = _STATUS_NAMES.get(status, str(status))
+    if status == 1:
+        raise IndexError(msg)
+    if status == 2:
+        raise ValueError(msg)
+    raise RuntimeError(f"psgd error {name}: {msg}")
+
+
+def shape_arrays(shapes: Sequence[Sequence[int]]):
+    flat: List[int] = [int(d) for s in shapes for d in s]
+    dims = (_i64 * max(1, len(flat)))(*flat)
+    ndims = (_i32 * max(1, len(shapes)))(*[len(s) for s in shapes])
+    return dims, ndims
+
+
+def ptr_array(ptrs: Sequence[int]):
+    return (_vp * max(1, len(ptrs)))(*ptrs)
+
+
+class Plan:
+    """Owns a psgd_plan handle (host layout only; device memory is bound by the caller)."""
+
+    def __init__(self, shapes: Sequence[Sequence[int]], rank: int, iters: int, dtype_code: int):
+        L = lib()
+        dims, ndims = shape_arrays(shapes)
+        h = _vp()
+        check(L.psgd_plan_create(dims, ndims, len(shapes), rank, iters, dtype_code, ctypes.byref(h)))
+        self._h = h
+        self.num_tensors = len(shapes)
+        self.iters = iters
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.psgd_plan_destroy(h)
+            self._h = None
+
+    # --- layout queries
+    def groups(self):
+        L, n_ = lib(), _i32()
+        check(L.psgd_plan_num_groups(self._h, ctypes.byref(n_)))
+        out = []
+        for g in range(n_.value):
+            n, m, r, c = _i64(), _i64(), _i32(), _i32()
+            check(L.psgd_plan_group(self._h, g, ctypes.byref(n), ctypes.byref(m), ctypes.byref(r), ctypes.byref(c)))
+            out.append((n.value, m.value, r.value, c.value))
+        return out
+
+    def factor_numel(self):
+        p, q = _i64(), _i64()
+        check(lib().psgd_plan_factor_numel(self._h, ctypes.byref(p), ctypes.byref(q)))
+        return p.value, q.value
+
+    def output_numel(self) -> int:
+        n = _i64()
+        check(lib().psgd_plan_output_numel(self._h, ctypes.byref(n)))
+        return n.value
+
+    def output_offsets(self) -> List[int]:
+        out, o = [], _i64()
+        for i in range(self.num_tensors):
+            check(lib().psgd_plan_output_offset(self._h, i, ctypes.byref(o)))
+            out.append(o.value)
+        return out
+
+    def workspace_bytes(self) -> int:
+        b = _i64()
+        check(lib().psgd_plan_workspace_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def compression_rate(self):
+        r, u, c = _dbl(), _dbl(), _dbl()
+        check(lib().psgd_plan_compression_rate(self._h, ctypes.byref(r), ctypes.byref(u), ctypes.byref(c)))
+        return r.value, u.value, c.value
+
+    # --- device
+    def bind(self, device: int, p_ptr: int, q_ptr: int, ws_ptr: int) -> None:
+        check(lib().psgd_plan_bind(self._h, device, p_ptr, q_ptr, ws_ptr))
+
+    def out_factor(self, step: int, it: int) -> int:
+        w = _i32()
+        check(lib().psgd_out_factor(self._h, step, it, ctypes.byref(w)))
+        return w.value
+
+    def compress(self, grads, step: int, it: int, stream: int) -> None:
+        check(lib().psgd_compress(self._h, grads, step, it, stream))
+
+    def decompress(self, grads, out_ptr: int, step: int, world: int, stream: int) -> None:
+        check(lib().psgd_decompress(self._h, grads, out_ptr, step, world, stream))
+
+    def aggregate(self, grads, out_ptr: int, step: int, stream: int) -> None:
+        check(lib().psgd_aggregate(self._h, grads, out_ptr, step, stream))
+
+
+class FlatPlan:
+    def __init__(self, numels: Sequence[int], dtype_code: int):
+        L = lib()
+        arr = (_i64 * max(1, len(numels)))(*numels)
+        h = _vp()
+        check(L.psgd_flat_create(arr, len(numels), dtype_code, ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.psgd_flat_destroy(h)
+            self._h = None
+
+    def workspace_bytes(self) -> int:
+        b = _i64()
+        check(lib().psgd_flat_workspace_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def bind(self, device: int, ws_ptr: int) -> None:
+        check(lib().psgd_flat_bind(self._h, device, ws_ptr))
+
+    def pack(self, tensors, flat_ptr: int, world: int, stream: int) -> None:
+        check(lib().psgd_flat_pack(self._h, tensors, flat_ptr, world, stream))
+
+
+def should_compress(shape: Sequence[int], rank: int, iters: int, min_rate: float) -> bool:
+    dims, _ = shape_arrays([shape])
+    out = _i32()
+    check(lib().psgd_should_compress(dims, len(shape), rank, iters, float(min_rate), ctypes.byref(out)))
+    return bool(out.value)

@@ -1,0 +1,117 @@
+// Internal layout shared by the host plan (psgd_plan.cpp) and the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psgd {
+
+constexpr int kMaxTerms = 16;   // == PSGD_MAX_ITERS
+constexpr int kBlock = 256;     // threads per workgroup for the streaming kernels
+constexpr int kWaves = kBlock / 64;
+
+// One compressed matrix (the [n, m] view of a tensor). Stored in GROUP order, so the
+// P/Q offsets below are monotone and reproduce the reference's _ps/_qs_buffer layout.
+struct MatDesc {
+    int64_t n, m;
+    int64_t poff, qoff;     // offsets (floats) of this matrix's P [n,r] / Q [m,r] panels
+    int64_t out_off;        // element offset in the flat output buffer
+    int64_t part_even;      // column partials [nchunk][m][r] (even iterations)
+    int64_t part_odd;       // row partials    [nstrip][n][r] (odd iterations)
+    int32_t r;
+    int32_t tensor;         // index into the gradient pointer table
+    int32_t group;
+    int32_t vec;            // 1: 4-element vector loads/stores (m % 4 == 0, aligned)
+    int32_t lanes;          // L: lanes sharing one row inside a wave (power of two <= 64)
+    int32_t nstrip;         // column strips of L*V columns
+    int32_t nchunk;         // row chunks
+    int32_t chunk_rows;     // rows per chunk (multiple of the block's rows per pass)
+};
+
+// Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
+struct Tile {
+    int32_t mat, strip, chunk, pad;
+};
+
+// Reduction item for the partial-sum pass: 256 consecutive factor elements of one matrix.
+struct RedItem {
+    int32_t mat, start;
+};
+
+// Orthonormalisation unit: rank 1 -> one shape GROUP (joint norm over count*k values);
+// rank > 1 -> one matrix (Householder QR of a k x r panel).
+struct OrthUnit {
+    int64_t off;    // offset (floats) in the P- or Q-layout buffer
+    int64_t k;      // rows of each panel
+    int32_t r;
+    int32_t count;  // panels in the unit (group size for rank 1, 1 otherwise)
+};
+
+// A list of rank-r terms  P_k Q_k^T : P-layout [n,r] and Q-layout [m,r] panel buffers.
+struct Terms {
+    const float* p[kMaxTerms];
+    const float* q[kMaxTerms];
+};
+
+struct ProductArgs {
+    const MatDesc* mats;
+    const Tile* tiles;
+    void* const* grads;
+    const float* x;      // orthonormal in-factor: P-layout (even) / Q-layout (odd)
+    float* part;         // partial-sum workspace
+    Terms res;           // error-feedback terms applied on the fly
+    int32_t nres;
+};
+
+struct ApplyArgs {
+    const MatDesc* mats;
+    const Tile* tiles;
+    void* const* grads;  // in: G_0, out: residual
+    void* out;           // flat output buffer
+    Terms res;           // local terms (residual)
+    Terms apx;           // all-reduced terms (approximation), scaled by alpha
+    int32_t nterms;
+    float alpha;         // 1 / world_size
+};
+
+struct ReduceArgs {
+    const MatDesc* mats;
+    const RedItem* items;
+    const float* part;
+    float* yloc;         // history copy of the local factor
+    float* state;        // reference-visible state buffer (the out-factor)
+    int32_t even;
+};
+
+struct OrthArgs {
+    const OrthUnit* units;
+    float* state;        // in-factor state buffer, orthonormalised in place
+    float* hx;           // history copy of the orthonormal in-factor
+    float* save;         // if non-null: copy of the pre-orthonormalisation values
+};
+
+struct FlatEntry {
+    int64_t off, numel;  // dense offset in the flat buffer (non-empty tensors only)
+    int64_t tensor;      // index into the pointer table
+    int64_t pad;
+};
+
+struct FlatArgs {
+    const FlatEntry* entries;
+    void* const* tensors;
+    void* flat;
+    int32_t count;
+    int32_t world;
+    int64_t total;
+};
+
+// Host-side launchers (psgd_kernels*.hip). Return hipError_t.
+hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a,
+                          int ntiles, hipStream_t s);
+hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a,
+                        int ntiles, hipStream_t s);
+hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
+hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_panel_floats, hipStream_t s);
+hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
+
+}  // namespace psgd

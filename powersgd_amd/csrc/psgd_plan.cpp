@@ -1,0 +1,621 @@
+// Host side of libpsgd: the codec plan (layout of groups, factor buffers, tiles) and the
+// C ABI declared in include/psgd.h. No torch: plain pointers, hipStream_t as void*.
+//
+// Layout mirrors the reference exactly where it is observable:
+//   - matrices = tensor.view(shape[0], -1), grouped by matrix shape in first-appearance order
+//     (reference powersgd/powersgd.py:253-263, :283-289);
+//   - P state = concat over groups of [count, n, r], Q state = concat of [count, m, r],
+//     r = min(rank, n, m) (:130-144, :237-251);
+//   - iteration parity = (step * num_iters_per_step + it) % 2 (:174).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "psgd.h"
+#include "psgd_internal.h"
+
+namespace psgd {
+hipError_t launch_product_f32(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_product_bf16(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_apply_f32(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_apply_bf16(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
+
+hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a, int ntiles,
+                          hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_product_f32(R, even, nres, a, ntiles, s)
+                             : launch_product_bf16(R, even, nres, a, ntiles, s);
+}
+hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a, int ntiles,
+                        hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_apply_f32(R, nterms, shared, a, ntiles, s)
+                             : launch_apply_bf16(R, nterms, shared, a, ntiles, s);
+}
+}  // namespace psgd
+
+using namespace psgd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define PSGD_HIP(expr)                                                                   \
+    do {                                                                                 \
+        const hipError_t e_ = (expr);                                                    \
+        if (e_ != hipSuccess)                                                            \
+            return fail(PSGD_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+int64_t pow2ceil(int64_t x) {
+    int64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int64_t env_int(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return std::atoll(v);
+}
+
+struct Geom {
+    int lanes, nstrip, nchunk, chunk_rows;
+    int64_t part_even, part_odd, ntiles;
+};
+
+// Tile geometry of one matrix for a vector width (see psgd_stream.cuh).
+Geom geometry(int64_t n, int64_t m, int r, int vec, int64_t tile_elems) {
+    const int V = vec ? 4 : 1;
+    const int64_t nq = (m + V - 1) / V;
+    Geom g;
+    g.lanes = int(std::min<int64_t>(64, pow2ceil(nq)));
+    const int rows_pass = kWaves * (64 / g.lanes);
+    g.nstrip = int((nq + g.lanes - 1) / g.lanes);
+    int64_t cr = tile_elems / (int64_t(g.lanes) * V);
+    cr = std::max<int64_t>(cr, rows_pass);
+    cr = round_up(cr, rows_pass);
+    cr = std::min(cr, round_up(n, rows_pass));
+    g.chunk_rows = int(cr);
+    g.nchunk = int((n + cr - 1) / cr);
+    g.part_even = int64_t(g.nchunk) * m * r;
+    g.part_odd = int64_t(g.nstrip) * n * r;
+    g.ntiles = int64_t(g.nchunk) * g.nstrip;
+    return g;
+}
+
+struct DevScope {  // make `dev` current for the scope, restore afterwards
+    int prev = -1;
+    explicit DevScope(int dev) {
+        (void)hipGetDevice(&prev);
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DevScope() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct psgd_plan {
+    int rank = 0, iters = 0, dtype = 0;
+    std::vector<std::vector<int64_t>> shapes;
+    struct Group {
+        int64_t n, m;
+        int r;
+        std::vector<int> tensors;
+        int64_t poff, qoff;
+    };
+    std::vector<Group> groups;
+    std::vector<MatDesc> mats;  // group order
+    std::vector<int> base_vec;  // vector path possible by shape (m % 4 == 0, r <= 8)
+    std::vector<int> vec_now;   // currently active vector flags
+    std::vector<int64_t> out_off;
+    int64_t out_total = 0, ptot = 0, qtot = 0, fmax = 0;
+    int rbucket = 1;
+    int64_t tile_elems = 16384;
+    std::vector<Tile> tiles;
+    int64_t tiles_cap = 0;
+    std::vector<RedItem> red_even, red_odd;
+    std::vector<OrthUnit> units_p, units_q;
+    int64_t panel_p = 0, panel_q = 0;
+    int64_t part_floats = 0;
+    double unc_floats = 0, comp_floats = 0;
+    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_red_even = 0, o_red_odd = 0, o_units_p = 0,
+           o_units_q = 0, o_hist = 0, o_part = 0, ws_bytes = 0;
+    bool bound = false;
+    int device = -1;
+    float* P = nullptr;
+    float* Q = nullptr;
+    char* ws = nullptr;
+    std::vector<void*> host_ptrs;
+
+    float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
+        return reinterpret_cast<float*>(ws + o_hist) + (int64_t(which) * iters + k) * fmax;
+    }
+    template <typename T>
+    T* dev(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+    bool even(int64_t step, int it) const { return ((step * iters + it) % 2) == 0; }
+
+    void set_vec(const std::vector<int>& vec) {
+        vec_now = vec;
+        tiles.clear();
+        for (size_t i = 0; i < mats.size(); ++i) {
+            MatDesc& d = mats[i];
+            const Geom g = geometry(d.n, d.m, d.r, vec[i], tile_elems);
+            d.vec = vec[i];
+            d.lanes = g.lanes;
+            d.nstrip = g.nstrip;
+            d.nchunk = g.nchunk;
+            d.chunk_rows = g.chunk_rows;
+            for (int c = 0; c < g.nchunk; ++c)
+                for (int s = 0; s < g.nstrip; ++s) tiles.push_back(Tile{int32_t(i), s, c, 0});
+        }
+    }
+};
+
+struct psgd_flat {
+    int dtype = 0;
+    std::vector<FlatEntry> entries;  // non-empty tensors only
+    int32_t count = 0;
+    int64_t total = 0;
+    size_t o_ptrs = 0, o_ents = 0, ws_bytes = 0;
+    bool bound = false;
+    int device = -1;
+    char* ws = nullptr;
+    std::vector<void*> host_ptrs;
+};
+
+namespace {
+
+int upload(void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return PSGD_OK;
+    PSGD_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return PSGD_OK;
+}
+
+// Upload the gradient pointer table when it changed; switch matrices whose gradient is not
+// vector-aligned to the scalar path (rare: views into unaligned flat buffers).
+int refresh_pointers(psgd_plan* p, void* const* grads, hipStream_t stream) {
+    const size_t nt = p->shapes.size();
+    bool same = p->host_ptrs.size() == nt;
+    for (size_t i = 0; same && i < nt; ++i) same = p->host_ptrs[i] == grads[i];
+    if (same) return PSGD_OK;
+    for (size_t i = 0; i < nt; ++i)
+        if (!grads[i]) return fail(PSGD_ERR_VALUE, "null gradient pointer");
+    std::vector<int> vec(p->mats.size());
+    const uintptr_t need = p->dtype == PSGD_F32 ? 16 : 8;
+    for (size_t i = 0; i < p->mats.size(); ++i)
+        vec[i] = p->base_vec[i] && (reinterpret_cast<uintptr_t>(grads[p->mats[i].tensor]) % need == 0);
+    PSGD_HIP(hipStreamSynchronize(stream));  // earlier launches may still read the tables
+    if (vec != p->vec_now) {
+        p->set_vec(vec);
+        if (int st = upload(p->dev<void>(p->o_mats), p->mats.data(), p->mats.size() * sizeof(MatDesc))) return st;
+        if (int st = upload(p->dev<void>(p->o_tiles), p->tiles.data(), p->tiles.size() * sizeof(Tile))) return st;
+    }
+    p->host_ptrs.assign(grads, grads + nt);
+    return upload(p->dev<void>(p->o_ptrs), p->host_ptrs.data(), nt * sizeof(void*));
+}
+
+void fill_terms(const psgd_plan* p, int64_t step, int count, Terms& res) {
+    for (int j = 0; j < count; ++j) {
+        const bool e = p->even(step, j);
+        // local rank-r term of iteration j: even -> (P_j = X_j, Q_j = Y_j); odd -> (P_j = Y_j, Q_j = X_j)
+        res.p[j] = e ? p->hist(0, j) : p->hist(1, j);
+        res.q[j] = e ? p->hist(1, j) : p->hist(0, j);
+    }
+    for (int j = count; j < kMaxTerms; ++j) res.p[j] = res.q[j] = nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int psgd_version(void) { return 100; }
+
+const char* psgd_last_error(void) { return g_err.c_str(); }
+
+int psgd_should_compress(const int64_t* shape, int32_t ndim, int32_t rank, int32_t iters,
+                         double min_rate, int32_t* out) {
+    if (!shape || !out || ndim < 1) return fail(PSGD_ERR_VALUE, "shape must have at least one dim");
+    int64_t numel = 1, sum = 0, mn = shape[0];
+    for (int i = 0; i < ndim; ++i) {
+        numel *= shape[i];
+        sum += shape[i];
+        mn = std::min(mn, shape[i]);
+    }
+    const double r = double(std::min<int64_t>(rank, mn));
+    const double avg = 0.5 * double(iters) * r * double(sum);  // reference :292-294
+    if (avg == 0.0) return fail(PSGD_ERR_VALUE, "zero average compressed size (division by zero)");
+    *out = (double(numel) / avg > min_rate) ? 1 : 0;  // reference :101-105
+    return PSGD_OK;
+}
+
+int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tensors, int32_t rank,
+                     int32_t iters, int32_t dtype, psgd_plan** out_plan) {
+    if (!out_plan) return fail(PSGD_ERR_VALUE, "out_plan is null");
+    *out_plan = nullptr;
+    if (num_tensors < 1 || !dims || !ndims) return fail(PSGD_ERR_INDEX, "list index out of range (no tensors)");
+    if (rank < 1) return fail(PSGD_ERR_VALUE, "rank must be >= 1");
+    if (iters < 1 || iters > PSGD_MAX_ITERS) return fail(PSGD_ERR_VALUE, "num_iters_per_step must be in [1, 16]");
+    if (dtype != PSGD_F32 && dtype != PSGD_BF16) return fail(PSGD_ERR_DTYPE, "dtype must be fp32 or bf16");
+
+    auto* p = new psgd_plan();
+    p->rank = rank;
+    p->iters = iters;
+    p->dtype = dtype;
+    p->tile_elems = std::max<int64_t>(1024, env_int("PSGD_TILE_ELEMS", 16384));
+    std::map<std::pair<int64_t, int64_t>, int> gid;
+    const int64_t* d = dims;
+    for (int t = 0; t < num_tensors; ++t) {
+        const int nd = ndims[t];
+        if (nd < 1) {
+            delete p;
+            return fail(PSGD_ERR_INDEX, "tuple index out of range (0-dim tensor)");
+        }
+        std::vector<int64_t> s(d, d + nd);
+        d += nd;
+        int64_t numel = 1;
+        for (int64_t x : s) numel *= x;
+        if (numel <= 0) {
+            delete p;
+            return fail(PSGD_ERR_LAYOUT, "cannot view an empty tensor as a matrix");
+        }
+        const int64_t n = s[0], m = numel / n;
+        auto key = std::make_pair(n, m);
+        auto it = gid.find(key);
+        if (it == gid.end()) {
+            it = gid.emplace(key, int(p->groups.size())).first;
+            psgd_plan::Group g;
+            g.n = n;
+            g.m = m;
+            g.r = int(std::min<int64_t>(rank, std::min(n, m)));
+            g.poff = g.qoff = 0;
+            p->groups.push_back(g);
+        }
+        p->groups[it->second].tensors.push_back(t);
+        p->shapes.push_back(std::move(s));
+        // compression_rate bookkeeping (reference :265-275, on the ORIGINAL shape)
+        int64_t sum = 0, mn = p->shapes.back()[0];
+        for (int64_t x : p->shapes.back()) {
+            sum += x;
+            mn = std::min(mn, x);
+        }
+        p->unc_floats += double(numel);
+        p->comp_floats += 0.5 * iters * double(std::min<int64_t>(rank, mn)) * double(sum);
+    }
+    int maxr = 1;
+    for (auto& g : p->groups) maxr = std::max(maxr, g.r);
+    if (maxr > 32) {
+        delete p;
+        return fail(PSGD_ERR_VALUE, "effective rank above 32 is not supported by this build");
+    }
+    p->rbucket = int(pow2ceil(maxr));
+
+    // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
+    // whose segment is not 16-byte aligned takes the scalar path
+    p->out_off.assign(num_tensors, 0);
+    for (int t = 0; t < num_tensors; ++t) {
+        int64_t numel = 1;
+        for (int64_t x : p->shapes[t]) numel *= x;
+        p->out_off[t] = p->out_total;
+        p->out_total += numel;
+    }
+    int64_t poff = 0, qoff = 0;
+    for (size_t gi = 0; gi < p->groups.size(); ++gi) {
+        auto& g = p->groups[gi];
+        g.poff = poff;
+        g.qoff = qoff;
+        for (size_t b = 0; b < g.tensors.size(); ++b) {
+            MatDesc md{};
+            md.n = g.n;
+            md.m = g.m;
+            md.r = g.r;
+            md.poff = poff + int64_t(b) * g.n * g.r;
+            md.qoff = qoff + int64_t(b) * g.m * g.r;
+            md.out_off = p->out_off[g.tensors[b]];
+            md.tensor = g.tensors[b];
+            md.group = int(gi);
+            p->mats.push_back(md);
+            p->base_vec.push_back((g.m % 4 == 0 && g.r <= 8 && md.out_off % 4 == 0) ? 1 : 0);
+        }
+        poff += int64_t(g.tensors.size()) * g.n * g.r;
+        qoff += int64_t(g.tensors.size()) * g.m * g.r;
+        // orthonormalisation units (reference orthogonalize() is called per group batch, :188)
+        if (g.r == 1) {
+            p->units_p.push_back(OrthUnit{g.poff, g.n, 1, int32_t(g.tensors.size())});
+            p->units_q.push_back(OrthUnit{g.qoff, g.m, 1, int32_t(g.tensors.size())});
+        } else {
+            for (size_t b = 0; b < g.tensors.size(); ++b) {
+                p->units_p.push_back(OrthUnit{g.poff + int64_t(b) * g.n * g.r, g.n, g.r, 1});
+                p->units_q.push_back(OrthUnit{g.qoff + int64_t(b) * g.m * g.r, g.m, g.r, 1});
+            }
+            p->panel_p = std::max(p->panel_p, g.n * g.r);
+            p->panel_q = std::max(p->panel_q, g.m * g.r);
+        }
+    }
+    p->ptot = poff;
+    p->qtot = qoff;
+    p->fmax = std::max(poff, qoff);
+
+    // partial-sum slabs sized for either vector width; reduction items
+    for (size_t i = 0; i < p->mats.size(); ++i) {
+        MatDesc& md = p->mats[i];
+        const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
+        const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
+        md.part_even = p->part_floats;
+        p->part_floats += std::max(a.part_even, b.part_even);
+        md.part_odd = p->part_floats;
+        p->part_floats += std::max(a.part_odd, b.part_odd);
+        p->tiles_cap += std::max(a.ntiles, b.ntiles);
+        for (int64_t s = 0; s < md.m * md.r; s += kBlock) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
+        for (int64_t s = 0; s < md.n * md.r; s += kBlock) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
+    }
+    p->set_vec(p->base_vec);
+
+    size_t off = 0;
+    auto carve = [&](size_t bytes) {
+        const size_t o = off;
+        off = align256(off + bytes);
+        return o;
+    };
+    p->o_ptrs = carve(size_t(num_tensors) * sizeof(void*));
+    p->o_mats = carve(p->mats.size() * sizeof(MatDesc));
+    p->o_tiles = carve(size_t(p->tiles_cap) * sizeof(Tile));
+    p->o_red_even = carve(p->red_even.size() * sizeof(RedItem));
+    p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
+    p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
+    p->o_units_q = carve(p->units_q.size() * sizeof(OrthUnit));
+    p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * sizeof(float));
+    p->o_part = carve(size_t(p->part_floats) * sizeof(float));
+    p->ws_bytes = off;
+    *out_plan = p;
+    return PSGD_OK;
+}
+
+int psgd_plan_destroy(psgd_plan* plan) {
+    delete plan;
+    return PSGD_OK;
+}
+
+int psgd_plan_num_groups(const psgd_plan* p, int32_t* out) {
+    if (!p || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    *out = int32_t(p->groups.size());
+    return PSGD_OK;
+}
+
+int psgd_plan_group(const psgd_plan* p, int32_t g, int64_t* n, int64_t* m, int32_t* r, int32_t* count) {
+    if (!p || g < 0 || g >= int32_t(p->groups.size())) return fail(PSGD_ERR_VALUE, "group index out of range");
+    const auto& gr = p->groups[g];
+    if (n) *n = gr.n;
+    if (m) *m = gr.m;
+    if (r) *r = gr.r;
+    if (count) *count = int32_t(gr.tensors.size());
+    return PSGD_OK;
+}
+
+int psgd_plan_factor_numel(const psgd_plan* p, int64_t* pn, int64_t* qn) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (pn) *pn = p->ptot;
+    if (qn) *qn = p->qtot;
+    return PSGD_OK;
+}
+
+int psgd_plan_output_offset(const psgd_plan* p, int32_t i, int64_t* off) {
+    if (!p || !off || i < 0 || i >= int32_t(p->out_off.size())) return fail(PSGD_ERR_VALUE, "tensor index out of range");
+    *off = p->out_off[i];
+    return PSGD_OK;
+}
+
+int psgd_plan_output_numel(const psgd_plan* p, int64_t* numel) {
+    if (!p || !numel) return fail(PSGD_ERR_VALUE, "null argument");
+    *numel = p->out_total;
+    return PSGD_OK;
+}
+
+int psgd_plan_workspace_bytes(const psgd_plan* p, int64_t* bytes) {
+    if (!p || !bytes) return fail(PSGD_ERR_VALUE, "null argument");
+    *bytes = int64_t(p->ws_bytes);
+    return PSGD_OK;
+}
+
+int psgd_plan_compression_rate(const psgd_plan* p, double* rate, double* unc, double* comp) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (rate) *rate = p->unc_floats / p->comp_floats;
+    if (unc) *unc = p->unc_floats;
+    if (comp) *comp = p->comp_floats;
+    return PSGD_OK;
+}
+
+int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* workspace) {
+    if (!p || !P || !Q || !workspace) return fail(PSGD_ERR_VALUE, "null argument");
+    if (reinterpret_cast<uintptr_t>(workspace) % 16) return fail(PSGD_ERR_LAYOUT, "workspace must be 16-byte aligned");
+    DevScope scope(device);
+    p->device = device;
+    p->P = P;
+    p->Q = Q;
+    p->ws = static_cast<char*>(workspace);
+    p->host_ptrs.clear();
+    if (int st = upload(p->dev<void>(p->o_mats), p->mats.data(), p->mats.size() * sizeof(MatDesc))) return st;
+    if (int st = upload(p->dev<void>(p->o_tiles), p->tiles.data(), p->tiles.size() * sizeof(Tile))) return st;
+    if (int st = upload(p->dev<void>(p->o_red_even), p->red_even.data(), p->red_even.size() * sizeof(RedItem))) return st;
+    if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
+    if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
+    if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
+    p->bound = true;
+    return PSGD_OK;
+}
+
+int psgd_out_factor(const psgd_plan* p, int64_t step, int32_t it, int32_t* which) {
+    if (!p || !which) return fail(PSGD_ERR_VALUE, "null argument");
+    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
+    *which = p->even(step, it) ? 0 : 1;
+    return PSGD_OK;
+}
+
+int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, void* stream) {
+    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    const bool even = p->even(step, it);
+    float* in = even ? p->P : p->Q;
+    float* out = even ? p->Q : p->P;
+
+    OrthArgs oa{};
+    oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
+    oa.state = in;
+    oa.hx = p->hist(0, it);
+    oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
+    const int nunits = int(even ? p->units_p.size() : p->units_q.size());
+    PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+
+    ProductArgs pa{};
+    pa.mats = p->dev<MatDesc>(p->o_mats);
+    pa.tiles = p->dev<Tile>(p->o_tiles);
+    pa.grads = p->dev<void* const>(p->o_ptrs);
+    pa.x = p->hist(0, it);
+    pa.part = p->dev<float>(p->o_part);
+    fill_terms(p, step, it, pa.res);
+    pa.nres = it;
+    PSGD_HIP(launch_product(p->dtype, p->rbucket, even, it, pa, int(p->tiles.size()), s));
+
+    ReduceArgs ra{};
+    ra.mats = pa.mats;
+    ra.items = p->dev<RedItem>(even ? p->o_red_even : p->o_red_odd);
+    ra.part = pa.part;
+    ra.yloc = p->hist(1, it);
+    ra.state = out;
+    ra.even = even ? 1 : 0;
+    const int nitems = int(even ? p->red_even.size() : p->red_odd.size());
+    PSGD_HIP(launch_reduce(ra, nitems, s));
+    return PSGD_OK;
+}
+
+int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
+                    void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0 || world < 1) return fail(PSGD_ERR_VALUE, "step/world size out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    const int I = p->iters;
+    ApplyArgs aa{};
+    aa.mats = p->dev<MatDesc>(p->o_mats);
+    aa.tiles = p->dev<Tile>(p->o_tiles);
+    aa.grads = p->dev<void* const>(p->o_ptrs);
+    aa.out = out;
+    fill_terms(p, step, I, aa.res);
+    float* last = p->even(step, I - 1) ? p->Q : p->P;  // all-reduced factor of the last iteration
+    for (int k = 0; k < kMaxTerms; ++k) aa.apx.p[k] = aa.apx.q[k] = nullptr;
+    for (int k = 0; k < I; ++k) {
+        const bool e = p->even(step, k);
+        float* ybar = k + 1 < I ? p->hist(2, k) : last;
+        aa.apx.p[k] = e ? p->hist(0, k) : ybar;
+        aa.apx.q[k] = e ? ybar : p->hist(0, k);
+    }
+    aa.nterms = I;
+    aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
+    PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
+    return PSGD_OK;
+}
+
+int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, void* stream) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    for (int it = 0; it < p->iters; ++it)
+        if (int st = psgd_compress(p, grads, step, it, stream)) return st;
+    return psgd_decompress(p, grads, out, step, 1, stream);
+}
+
+// ------------------------------------------------------------------ flat pack ------
+int psgd_flat_create(const int64_t* numels, int32_t count, int32_t dtype, psgd_flat** out) {
+    if (!out) return fail(PSGD_ERR_VALUE, "null argument");
+    *out = nullptr;
+    if (count < 0 || (count > 0 && !numels)) return fail(PSGD_ERR_VALUE, "bad tensor list");
+    if (dtype != PSGD_F32 && dtype != PSGD_BF16) return fail(PSGD_ERR_DTYPE, "dtype must be fp32 or bf16");
+    auto* f = new psgd_flat();
+    f->dtype = dtype;
+    f->count = count;
+    for (int i = 0; i < count; ++i) {
+        if (numels[i] < 0) {
+            delete f;
+            return fail(PSGD_ERR_VALUE, "negative numel");
+        }
+        // empty tensors occupy no flat range: no lookup entry (their pointer slot stays)
+        if (numels[i] > 0) f->entries.push_back(FlatEntry{f->total, numels[i], i, 0});
+        f->total += numels[i];
+    }
+    f->o_ptrs = 0;
+    f->o_ents = align256(size_t(std::max(count, 1)) * sizeof(void*));
+    f->ws_bytes = align256(f->o_ents + size_t(std::max(count, 1)) * sizeof(FlatEntry));
+    *out = f;
+    return PSGD_OK;
+}
+
+int psgd_flat_destroy(psgd_flat* f) {
+    delete f;
+    return PSGD_OK;
+}
+
+int psgd_flat_workspace_bytes(const psgd_flat* f, int64_t* bytes) {
+    if (!f || !bytes) return fail(PSGD_ERR_VALUE, "null argument");
+    *bytes = int64_t(f->ws_bytes);
+    return PSGD_OK;
+}
+
+int psgd_flat_bind(psgd_flat* f, int32_t device, void* workspace) {
+    if (!f || !workspace) return fail(PSGD_ERR_VALUE, "null argument");
+    DevScope scope(device);
+    f->device = device;
+    f->ws = static_cast<char*>(workspace);
+    f->host_ptrs.clear();
+    if (int st = upload(f->ws + f->o_ents, f->entries.data(), f->entries.size() * sizeof(FlatEntry))) return st;
+    f->bound = true;
+    return PSGD_OK;
+}
+
+int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world, void* stream) {
+    if (!f || (!tensors && f->count > 0) || (!flat && f->total > 0)) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
+    if (world < 1) return fail(PSGD_ERR_VALUE, "world size must be >= 1");
+    if (f->total == 0) return PSGD_OK;
+    DevScope scope(f->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t n = size_t(f->count);
+    bool same = f->host_ptrs.size() == n;
+    for (size_t i = 0; same && i < n; ++i) same = f->host_ptrs[i] == tensors[i];
+    if (!same) {
+        PSGD_HIP(hipStreamSynchronize(s));
+        f->host_ptrs.assign(tensors, tensors + n);
+        if (int st = upload(f->ws + f->o_ptrs, f->host_ptrs.data(), n * sizeof(void*))) return st;
+    }
+    FlatArgs a{};
+    a.entries = reinterpret_cast<const FlatEntry*>(f->ws + f->o_ents);
+    a.tensors = reinterpret_cast<void* const*>(f->ws + f->o_ptrs);
+    a.flat = flat;
+    a.count = int32_t(f->entries.size());
+    a.world = world;
+    a.total = f->total;
+    PSGD_HIP(launch_flat_pack(f->dtype, a, s));
+    return PSGD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,8 @@
+// Instantiations of the product kernels for bf16_t gradients (see psgd_stream.cuh).
+#include "psgd_stream.cuh"
+
+namespace psgd {
+hipError_t launch_product_bf16(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+    return dispatch_product<bf16_t>(R, even, nres, a, ntiles, s);
+}
+}  // namespace psgd

@@ -1,0 +1,8 @@
+// Instantiations of the product kernels for float gradients (see psgd_stream.cuh).
+#include "psgd_stream.cuh"
+
+namespace psgd {
+hipError_t launch_product_f32(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+    return dispatch_product<float>(R, even, nres, a, ntiles, s);
+}
+}  // namespace psgd

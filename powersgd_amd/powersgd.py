@@ -1,0 +1,335 @@
+"""PowerSGD aggregators — the reference's Python interface over the MI355X HIP codec.
+
+Mirrors epfml/powersgd ``powersgd/powersgd.py`` (same class names, constructor
+arguments, attributes, return values and in-place side effects):
+
+* ``Aggregator``      reference :11-19
+* ``AllReduce``       reference :22-31   (flat pack/scale/zero kernel + all-reduce)
+* ``Config``          reference :34-38
+* ``PowerSGD``        reference :41-105  (warm-up, compression mask, split/merge)
+* ``BasicConfig``     reference :108-110
+* ``BasicPowerSGD``   reference :113-275 (the hot path: libpsgd.so, see include/psgd.h)
+
+Differences, all deliberate:
+* Device tensors on a ROCm GPU only; the HIP library is mandatory (no CPU fallback).
+* bfloat16 gradients are supported (the reference raises at its ``bmm``, :189): the
+  gradient matrix is read/written in bf16, factors and arithmetic stay fp32.
+* Returned compressed outputs are views of one flat buffer instead of separate
+  ``empty_like`` tensors (uncompressed outputs are views in the reference too). The
+  buffer is reused across steps only when its storage proves nobody else holds a
+  reference to it, so the reuse is not observable.
+"""
+from __future__ import annotations
+
+import sys
+from abc import ABC, abstractmethod
+from collections import defaultdict
+from typing import Dict, List, NamedTuple, Optional, Sequence, Union
+
+import torch
+
+from . import _lib
+from .utils import is_distributed
+
+_DTYPES = {torch.float32: _lib.PSGD_F32, torch.bfloat16: _lib.PSGD_BF16}
+
+
+def _require_device(device: torch.device) -> int:
+    if device.type != "cuda":
+        raise RuntimeError(
+            f"powersgd_amd runs its codec on MI355X GPUs (HIP); got tensors on '{device}'"
+        )
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def _dtype_code(dtype: torch.dtype) -> int:
+    try:
+        return _DTYPES[dtype]
+    except KeyError:
+        raise RuntimeError(f"powersgd_amd supports float32 and bfloat16 gradients, got {dtype}")
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class _OutputSlab:
+    """Flat output buffer + views, reused only while nothing outside holds them.
+
+    "Nothing holds them" = no Python reference to any returned view survives (refcounts
+    back to the cached baseline) AND no other tensor shares the storage (storage use
+    count back to baseline). Otherwise a fresh buffer is allocated, exactly like the
+    reference's per-call ``empty_like``.
+    """
+
+    def __init__(self):
+        self.flat: Optional[torch.Tensor] = None
+        self.views: List[torch.Tensor] = []
+        self._base_uses = 0
+        self._base_refs: List[int] = []
+
+    def _uses(self) -> int:
+        return torch._C._storage_Use_Count(self.flat.untyped_storage()._cdata)
+
+    def _refs(self) -> List[int]:
+        return [sys.getrefcount(v) for v in self.views]
+
+    def get(self, numel: int, like: Sequence[torch.Tensor], dtype, device) -> List[torch.Tensor]:
+        if self.flat is not None and self._uses() == self._base_uses and self._refs() == self._base_refs:
+            return list(self.views)
+        flat = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        self.views = list(torch._utils._unflatten_dense_tensors(flat[:numel], list(like)))
+        self.flat = flat
+        self._base_uses = self._uses()
+        self._base_refs = self._refs()
+        return list(self.views)
+
+
+class Aggregator(ABC):
+    """reference :11-19."""
+
+    @abstractmethod
+    def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
+        """Average ``gradients`` across workers; mutates them (zero, or the compression error)."""
+
+
+class AllReduce(Aggregator):
+    """Flat all-reduce average of uncompressed tensors (reference :22-31).
+
+    One HIP kernel copies every tensor (divided by the world size when distributed)
+    into a flat buffer and zeroes the inputs; the flat buffer is SUM-all-reduced and
+    the outputs are views of it, as in the reference.
+    """
+
+    def __init__(self):
+        self._plans: Dict[tuple, tuple] = {}
+        self._slab = _OutputSlab()
+
+    def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
+        if len(gradients) == 0:
+            return []
+        g0 = gradients[0]
+        dev_index = _require_device(g0.device)
+        dtype = g0.dtype
+        code = _dtype_code(dtype)
+        for g in gradients:
+            if g.dtype != dtype or g.device != g0.device:
+                raise RuntimeError("AllReduce expects tensors of one dtype on one device")
+            if not g.is_contiguous():
+                raise RuntimeError("view size is not compatible with input tensor's size and stride")
+        numels = tuple(g.numel() for g in gradients)
+        key = (numels, dtype, g0.device)
+        entry = self._plans.get(key)
+        if entry is None:
+            plan = _lib.FlatPlan(numels, code)
+            ws = torch.empty(plan.workspace_bytes(), dtype=torch.uint8, device=g0.device)
+            plan.bind(dev_index, ws.data_ptr())
+            entry = (plan, ws, _OutputSlab())
+            self._plans[key] = entry
+        plan, _, slab = entry
+        total = sum(numels)
+        outs = slab.get(total, gradients, dtype, g0.device)
+        world = torch.distributed.get_world_size() if is_distributed() else 1
+        ptrs = _lib.ptr_array([g.data_ptr() for g in gradients])
+        plan.pack(ptrs, slab.flat.data_ptr(), world, _stream(g0.device))
+        if is_distributed():
+            torch.distributed.all_reduce(slab.flat[:total])
+        return outs
+
+
+class Config(NamedTuple):
+    """reference :34-38 (same fields and defaults)."""
+
+    rank: int  # lower rank => more aggressive compression
+    min_compression_rate: float = 2  # skip compression on some gradients
+    num_iters_per_step: int = 1  # lower number => more aggressive compression
+    start_compressing_after_num_steps: int = 100
+
+
+class PowerSGD(Aggregator):
+    """Applies PowerSGD only after a configurable number of steps, and only on
+    parameters with strong compression (reference :41-105)."""
+
+    def __init__(self, params: List[torch.Tensor], config: Config):
+        self.config = config
+        self.device = list(params)[0].device
+        self.is_compressed_mask = [self._should_compress(p.shape) for p in params]
+        self.step_counter = 0
+        compressed_params, _ = self._split(params)
+        self._powersgd = BasicPowerSGD(
+            compressed_params,
+            config=BasicConfig(rank=config.rank, num_iters_per_step=config.num_iters_per_step),
+        )
+        self._allreduce = AllReduce()
+
+    def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
+        self.step_counter += 1
+        if self.step_counter <= self.config.start_compressing_after_num_steps:
+            return self._allreduce.aggregate(gradients)
+        compressed, uncompressed = self._split(gradients)
+        return self._merge(
+            self._powersgd.aggregate(compressed),
+            self._allreduce.aggregate(uncompressed),
+        )
+
+    def _split(self, params: List[torch.Tensor]):
+        comp, unc = [], []
+        for p, c in zip(params, self.is_compressed_mask):
+            (comp if c else unc).append(p)
+        return comp, unc
+
+    def _merge(self, compressed: List[torch.Tensor], uncompressed: List[torch.Tensor]) -> List[torch.Tensor]:
+        assert len(compressed) + len(uncompressed) == len(self.is_compressed_mask)
+        ci, ui = iter(compressed), iter(uncompressed)
+        return [next(ci) if c else next(ui) for c in self.is_compressed_mask]
+
+    def _should_compress(self, shape: torch.Size) -> bool:
+        return shape.numel() / avg_compressed_size(shape, self.config) > self.config.min_compression_rate
+
+
+class BasicConfig(NamedTuple):
+    """reference :108-110."""
+
+    rank: int  # lower rank => more aggressive compression
+    num_iters_per_step: int = 1  # lower number => more aggressive compression
+
+
+class BasicPowerSGD(Aggregator):
+    """PowerSGD codec on every given tensor (reference :113-275), on the HIP path.
+
+    State matches the reference: ``_ps_buffer``/``_qs_buffer`` (fp32, group-ordered
+    [B, n, r] / [B, m, r] batches) with views ``_ps``/``_qs``, ``step_counter``,
+    ``generator`` (seeded 0 on the params' device and drawn exactly as the reference).
+    """
+
+    def __init__(self, params: List[torch.Tensor], config: BasicConfig):
+        self.config = config
+        self.params = list(params)
+        self.device = self.params[0].device  # IndexError on an empty list, as the reference
+        self.dtype = self.params[0].dtype
+        self._dev_index = _require_device(self.device)
+        self._code = _dtype_code(self.dtype)
+        self.params_per_shape = self._matrices_per_shape(self.params)
+        self._plan = _lib.Plan([tuple(p.shape) for p in self.params], config.rank,
+                               config.num_iters_per_step, self._code)
+
+        self.generator = torch.Generator(device=self.device).manual_seed(0)
+        self.step_counter = 0
+        p_batches = [self._init_p_batch(s, ps) for s, ps in self.params_per_shape.items()]
+        q_batches = [self._init_q_batch(s, ps) for s, ps in self.params_per_shape.items()]
+        self._ps_buffer = torch.cat([b.view(-1) for b in p_batches])
+        self._qs_buffer = torch.cat([b.view(-1) for b in q_batches])
+        self._ps = _views(self._ps_buffer, [b.shape for b in p_batches])
+        self._qs = _views(self._qs_buffer, [b.shape for b in q_batches])
+        pn, qn = self._plan.factor_numel()
+        assert pn == self._ps_buffer.numel() and qn == self._qs_buffer.numel()
+        if self._ps_buffer.dtype != torch.float32:
+            raise RuntimeError("powersgd_amd keeps P/Q in float32 (torch default dtype must be float32)")
+        self._workspace = torch.empty(self._plan.workspace_bytes(), dtype=torch.uint8, device=self.device)
+        self._plan.bind(self._dev_index, self._ps_buffer.data_ptr(), self._qs_buffer.data_ptr(),
+                        self._workspace.data_ptr())
+        self._out_numel = self._plan.output_numel()
+        self._slab = _OutputSlab()
+        self._ptr_key: Optional[tuple] = None
+        self._ptr_arr = None
+        self._apply_events: Optional[list] = None  # set by bench.py to time k_apply
+
+    def _grad_pointers(self, gradients: List[torch.Tensor]):
+        key = tuple(g.data_ptr() for g in gradients)
+        if key != self._ptr_key:
+            if len(gradients) != len(self.params):
+                raise ValueError(f"expected {len(self.params)} gradients, got {len(gradients)}")
+            for g, p in zip(gradients, self.params):
+                if g.shape != p.shape:
+                    raise RuntimeError(f"gradient shape {tuple(g.shape)} != parameter shape {tuple(p.shape)}")
+                if g.dtype != self.dtype:
+                    raise RuntimeError(f"expected scalar type {self.dtype} but found {g.dtype}")
+                if g.device != self.device:
+                    raise RuntimeError(f"gradient on {g.device}, codec on {self.device}")
+                if not g.is_contiguous():
+                    raise RuntimeError("view size is not compatible with input tensor's size and stride")
+            self._ptr_key = key
+            self._ptr_arr = _lib.ptr_array(key)
+        return self._ptr_arr
+
+    def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
+        """reference :146-235. Mutates ``gradients`` into the compression error."""
+        ptrs = self._grad_pointers(gradients)
+        outs = self._slab.get(self._out_numel, gradients, self.dtype, self.device)
+        out_ptr = self._slab.flat.data_ptr()
+        stream = _stream(self.device)
+        step = self.step_counter
+        dist = is_distributed()
+        if dist or self._apply_events is not None:
+            world = torch.distributed.get_world_size() if dist else 1
+            for it in range(self.config.num_iters_per_step):
+                self._plan.compress(ptrs, step, it, stream)
+                if dist:
+                    buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
+                    torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
+            if self._apply_events is not None:  # bench.py: time the fused final kernel on its stream
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self._plan.decompress(ptrs, out_ptr, step, world, stream)
+                e1.record()
+                self._apply_events.append((e0, e1))
+            else:
+                self._plan.decompress(ptrs, out_ptr, step, world, stream)
+        else:
+            self._plan.aggregate(ptrs, out_ptr, step, stream)
+        self.step_counter += 1
+        return outs
+
+    def _init_p_batch(self, shape: torch.Size, params: List[torch.Tensor]) -> torch.Tensor:
+        rank = min(self.config.rank, min(shape))
+        return torch.randn([len(params), shape[0], rank], generator=self.generator, device=self.device)
+
+    def _init_q_batch(self, shape: torch.Size, params: List[torch.Tensor]) -> torch.Tensor:
+        rank = min(self.config.rank, min(shape))
+        return torch.randn([len(params), shape[1], rank], generator=self.generator, device=self.device)
+
+    @classmethod
+    def _matrices_per_shape(cls, tensors: List[torch.Tensor]) -> Dict[torch.Size, List[torch.Tensor]]:
+        shape2tensors: Dict[torch.Size, List[torch.Tensor]] = defaultdict(list)
+        for t in tensors:
+            m = view_as_matrix(t)
+            shape2tensors[m.shape].append(m)
+        return shape2tensors
+
+    @property
+    def uncompressed_num_floats(self) -> int:
+        return sum(p.shape.numel() for p in self.params)
+
+    @property
+    def compressed_num_floats(self) -> float:
+        return sum(avg_compressed_size(p.shape, self.config) for p in self.params)
+
+    @property
+    def compression_rate(self) -> float:
+        return self.uncompressed_num_floats / self.compressed_num_floats
+
+
+def _views(buf: torch.Tensor, shapes) -> List[torch.Tensor]:
+    out, i = [], 0
+    for s in shapes:
+        n = s.numel()
+        out.append(buf[i:i + n].view(s))
+        i += n
+    return out
+
+
+def batch_transpose(batch_of_matrices: torch.Tensor) -> torch.Tensor:
+    """reference :279-280."""
+    return batch_of_matrices.permute([0, 2, 1])
+
+
+def view_as_matrix(tensor: torch.Tensor) -> torch.Tensor:
+    """[output features, input features (x kernel dims)] view (reference :283-289)."""
+    return tensor.view(tensor.shape[0], -1)
+
+
+def avg_compressed_size(shape: torch.Size, config: Union[Config, BasicConfig]) -> float:
+    """reference :292-294 — on the ORIGINAL tensor shape."""
+    rank = min(config.rank, min(shape))
+    return 0.5 * config.num_iters_per_step * rank * sum(shape)
