@@ -26,6 +26,11 @@ struct MatDesc {
     int32_t nstrip;         // column strips of L*V columns
     int32_t nchunk;         // row chunks
     int32_t chunk_rows;     // rows per chunk (multiple of the block's rows per pass)
+    // odd iterations (P = G Q): MFMA tiles when odd_mfma, else the lane-column tiles above
+    int32_t odd_mfma;
+    int32_t odd_nstrip;     // column strips of the odd partials (reduce pass)
+    int32_t odd_sw;         // MFMA strip width (columns, multiple of 16)
+    int32_t odd_chunk_rows; // MFMA chunk rows (multiple of 16 * kWaves)
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
@@ -96,22 +101,31 @@ struct FlatEntry {
     int64_t pad;
 };
 
+// Flat-pack work item: kFlatItem consecutive elements of one entry.
+constexpr int kFlatItem = 8 * kBlock;
+struct FlatItem {
+    int32_t entry, pad;
+    int64_t start;
+};
+
 struct FlatArgs {
     const FlatEntry* entries;
+    const FlatItem* items;
     void* const* tensors;
     void* flat;
-    int32_t count;
+    int32_t nitems;
     int32_t world;
-    int64_t total;
 };
 
 // Host-side launchers (psgd_kernels*.hip). Return hipError_t.
 hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a,
                           int ntiles, hipStream_t s);
+hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int ntiles,
+                           hipStream_t s);
 hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a,
                         int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
-hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_panel_floats, hipStream_t s);
+hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
 
 }  // namespace psgd

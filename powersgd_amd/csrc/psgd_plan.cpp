@@ -26,6 +26,13 @@ hipError_t launch_product_f32(int R, bool even, int nres, const ProductArgs& a, 
 hipError_t launch_product_bf16(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_apply_f32(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_apply_bf16(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_odd_mfma_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_odd_mfma_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+
+hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_odd_mfma_f32(R, nres, a, ntiles, s)
+                             : launch_odd_mfma_bf16(R, nres, a, ntiles, s);
+}
 
 hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a, int ntiles,
                           hipStream_t s) {
@@ -85,6 +92,8 @@ Geom geometry(int64_t n, int64_t m, int r, int vec, int64_t tile_elems) {
     const int rows_pass = kWaves * (64 / g.lanes);
     g.nstrip = int((nq + g.lanes - 1) / g.lanes);
     int64_t cr = tile_elems / (int64_t(g.lanes) * V);
+    // a small matrix must still spread over several workgroups (its tile is a serial chain)
+    cr = std::min<int64_t>(cr, std::max<int64_t>(rows_pass, round_up((n + 7) / 8, rows_pass)));
     cr = std::max<int64_t>(cr, rows_pass);
     cr = round_up(cr, rows_pass);
     cr = std::min(cr, round_up(n, rows_pass));
@@ -93,6 +102,24 @@ Geom geometry(int64_t n, int64_t m, int r, int vec, int64_t tile_elems) {
     g.part_even = int64_t(g.nchunk) * m * r;
     g.part_odd = int64_t(g.nstrip) * n * r;
     g.ntiles = int64_t(g.nchunk) * g.nstrip;
+    return g;
+}
+
+struct OddGeom {
+    int sw, chunk_rows, nstrip, nchunk;
+};
+
+// MFMA odd-product tiles: strips of up to 256 columns (kOddSW, psgd_stream.cuh), chunks of
+// 64 * g rows (4 waves x 16-row groups x g) sized to about tile_elems elements.
+OddGeom odd_geometry(int64_t n, int64_t m, int64_t tile_elems) {
+    OddGeom g;
+    g.sw = int(std::min<int64_t>(256, round_up(m, 16)));
+    const int64_t rows_pass = 16 * kWaves;
+    int64_t groups = std::max<int64_t>(1, tile_elems / (rows_pass * g.sw));
+    int64_t cr = std::min(groups * rows_pass, round_up(n, rows_pass));
+    g.chunk_rows = int(cr);
+    g.nstrip = int((m + g.sw - 1) / g.sw);
+    g.nchunk = int((n + cr - 1) / cr);
     return g;
 }
 
@@ -128,15 +155,17 @@ struct psgd_plan {
     int64_t out_total = 0, ptot = 0, qtot = 0, fmax = 0;
     int rbucket = 1;
     int64_t tile_elems = 16384;
-    std::vector<Tile> tiles;
-    int64_t tiles_cap = 0;
+    std::vector<Tile> tiles;     // lane-column tiles of every matrix (even products, apply)
+    std::vector<Tile> tiles_ov;  // lane-column tiles of the odd-VALU matrices
+    std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
+    int64_t tiles_cap = 0, tiles_om_cap = 0;
     std::vector<RedItem> red_even, red_odd;
     std::vector<OrthUnit> units_p, units_q;
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_floats = 0;
     double unc_floats = 0, comp_floats = 0;
-    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_red_even = 0, o_red_odd = 0, o_units_p = 0,
-           o_units_q = 0, o_hist = 0, o_part = 0, ws_bytes = 0;
+    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_red_even = 0,
+           o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, ws_bytes = 0;
     bool bound = false;
     int device = -1;
     float* P = nullptr;
@@ -154,6 +183,9 @@ struct psgd_plan {
     void set_vec(const std::vector<int>& vec) {
         vec_now = vec;
         tiles.clear();
+        tiles_ov.clear();
+        tiles_om.clear();
+        const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         for (size_t i = 0; i < mats.size(); ++i) {
             MatDesc& d = mats[i];
             const Geom g = geometry(d.n, d.m, d.r, vec[i], tile_elems);
@@ -162,18 +194,36 @@ struct psgd_plan {
             d.nstrip = g.nstrip;
             d.nchunk = g.nchunk;
             d.chunk_rows = g.chunk_rows;
+            d.odd_mfma = (use_mfma && vec[i] && d.r <= 8) ? 1 : 0;
             for (int c = 0; c < g.nchunk; ++c)
-                for (int s = 0; s < g.nstrip; ++s) tiles.push_back(Tile{int32_t(i), s, c, 0});
+                for (int s = 0; s < g.nstrip; ++s) {
+                    tiles.push_back(Tile{int32_t(i), s, c, 0});
+                    if (!d.odd_mfma) tiles_ov.push_back(Tile{int32_t(i), s, c, 0});
+                }
+            if (d.odd_mfma) {
+                const OddGeom og = odd_geometry(d.n, d.m, tile_elems);
+                d.odd_sw = og.sw;
+                d.odd_chunk_rows = og.chunk_rows;
+                d.odd_nstrip = og.nstrip;
+                for (int c = 0; c < og.nchunk; ++c)
+                    for (int s = 0; s < og.nstrip; ++s) tiles_om.push_back(Tile{int32_t(i), s, c, 0});
+            } else {
+                d.odd_sw = d.odd_chunk_rows = 0;
+                d.odd_nstrip = g.nstrip;
+            }
         }
     }
+
+    int upload_tiles() const;
 };
 
 struct psgd_flat {
     int dtype = 0;
     std::vector<FlatEntry> entries;  // non-empty tensors only
+    std::vector<FlatItem> items;
     int32_t count = 0;
     int64_t total = 0;
-    size_t o_ptrs = 0, o_ents = 0, ws_bytes = 0;
+    size_t o_ptrs = 0, o_ents = 0, o_items = 0, ws_bytes = 0;
     bool bound = false;
     int device = -1;
     char* ws = nullptr;
@@ -204,12 +254,22 @@ int refresh_pointers(psgd_plan* p, void* const* grads, hipStream_t stream) {
     PSGD_HIP(hipStreamSynchronize(stream));  // earlier launches may still read the tables
     if (vec != p->vec_now) {
         p->set_vec(vec);
-        if (int st = upload(p->dev<void>(p->o_mats), p->mats.data(), p->mats.size() * sizeof(MatDesc))) return st;
-        if (int st = upload(p->dev<void>(p->o_tiles), p->tiles.data(), p->tiles.size() * sizeof(Tile))) return st;
+        if (int st = p->upload_tiles()) return st;
     }
     p->host_ptrs.assign(grads, grads + nt);
     return upload(p->dev<void>(p->o_ptrs), p->host_ptrs.data(), nt * sizeof(void*));
 }
+
+}  // namespace
+
+int psgd_plan::upload_tiles() const {
+    if (int st = upload(dev<void>(o_mats), mats.data(), mats.size() * sizeof(MatDesc))) return st;
+    if (int st = upload(dev<void>(o_tiles), tiles.data(), tiles.size() * sizeof(Tile))) return st;
+    if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
+    return upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile));
+}
+
+namespace {
 
 void fill_terms(const psgd_plan* p, int64_t step, int count, Terms& res) {
     for (int j = 0; j < count; ++j) {
@@ -344,8 +404,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
                 p->units_p.push_back(OrthUnit{g.poff + int64_t(b) * g.n * g.r, g.n, g.r, 1});
                 p->units_q.push_back(OrthUnit{g.qoff + int64_t(b) * g.m * g.r, g.m, g.r, 1});
             }
-            p->panel_p = std::max(p->panel_p, g.n * g.r);
-            p->panel_q = std::max(p->panel_q, g.m * g.r);
+            p->panel_p = std::max(p->panel_p, g.n);  // longest rank>1 panel (rows)
+            p->panel_q = std::max(p->panel_q, g.m);
         }
     }
     p->ptot = poff;
@@ -357,11 +417,13 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         MatDesc& md = p->mats[i];
         const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
         const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
+        const OddGeom og = odd_geometry(md.n, md.m, p->tile_elems);
         md.part_even = p->part_floats;
         p->part_floats += std::max(a.part_even, b.part_even);
         md.part_odd = p->part_floats;
-        p->part_floats += std::max(a.part_odd, b.part_odd);
+        p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
+        p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
         for (int64_t s = 0; s < md.m * md.r; s += kBlock) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
         for (int64_t s = 0; s < md.n * md.r; s += kBlock) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
     }
@@ -376,6 +438,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_ptrs = carve(size_t(num_tensors) * sizeof(void*));
     p->o_mats = carve(p->mats.size() * sizeof(MatDesc));
     p->o_tiles = carve(size_t(p->tiles_cap) * sizeof(Tile));
+    p->o_tiles_ov = carve(size_t(p->tiles_cap) * sizeof(Tile));
+    p->o_tiles_om = carve(size_t(std::max<int64_t>(p->tiles_om_cap, 1)) * sizeof(Tile));
     p->o_red_even = carve(p->red_even.size() * sizeof(RedItem));
     p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
@@ -450,8 +514,7 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     p->Q = Q;
     p->ws = static_cast<char*>(workspace);
     p->host_ptrs.clear();
-    if (int st = upload(p->dev<void>(p->o_mats), p->mats.data(), p->mats.size() * sizeof(MatDesc))) return st;
-    if (int st = upload(p->dev<void>(p->o_tiles), p->tiles.data(), p->tiles.size() * sizeof(Tile))) return st;
+    if (int st = p->upload_tiles()) return st;
     if (int st = upload(p->dev<void>(p->o_red_even), p->red_even.data(), p->red_even.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
@@ -494,7 +557,18 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
     pa.part = p->dev<float>(p->o_part);
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
-    PSGD_HIP(launch_product(p->dtype, p->rbucket, even, it, pa, int(p->tiles.size()), s));
+    if (even) {
+        PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, int(p->tiles.size()), s));
+    } else {
+        if (!p->tiles_ov.empty()) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_ov);
+            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, it, pa, int(p->tiles_ov.size()), s));
+        }
+        if (!p->tiles_om.empty()) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_om);
+            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 8), it, pa, int(p->tiles_om.size()), s));
+        }
+    }
 
     ReduceArgs ra{};
     ra.mats = pa.mats;
@@ -563,9 +637,12 @@ int psgd_flat_create(const int64_t* numels, int32_t count, int32_t dtype, psgd_f
         if (numels[i] > 0) f->entries.push_back(FlatEntry{f->total, numels[i], i, 0});
         f->total += numels[i];
     }
+    for (size_t e = 0; e < f->entries.size(); ++e)
+        for (int64_t st = 0; st < f->entries[e].numel; st += kFlatItem) f->items.push_back(FlatItem{int32_t(e), 0, st});
     f->o_ptrs = 0;
     f->o_ents = align256(size_t(std::max(count, 1)) * sizeof(void*));
-    f->ws_bytes = align256(f->o_ents + size_t(std::max(count, 1)) * sizeof(FlatEntry));
+    f->o_items = align256(f->o_ents + std::max<size_t>(f->entries.size(), 1) * sizeof(FlatEntry));
+    f->ws_bytes = align256(f->o_items + std::max<size_t>(f->items.size(), 1) * sizeof(FlatItem));
     *out = f;
     return PSGD_OK;
 }
@@ -588,6 +665,7 @@ int psgd_flat_bind(psgd_flat* f, int32_t device, void* workspace) {
     f->ws = static_cast<char*>(workspace);
     f->host_ptrs.clear();
     if (int st = upload(f->ws + f->o_ents, f->entries.data(), f->entries.size() * sizeof(FlatEntry))) return st;
+    if (int st = upload(f->ws + f->o_items, f->items.data(), f->items.size() * sizeof(FlatItem))) return st;
     f->bound = true;
     return PSGD_OK;
 }
@@ -609,11 +687,11 @@ int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world
     }
     FlatArgs a{};
     a.entries = reinterpret_cast<const FlatEntry*>(f->ws + f->o_ents);
+    a.items = reinterpret_cast<const FlatItem*>(f->ws + f->o_items);
     a.tensors = reinterpret_cast<void* const*>(f->ws + f->o_ptrs);
     a.flat = flat;
-    a.count = int32_t(f->entries.size());
+    a.nitems = int32_t(f->items.size());
     a.world = world;
-    a.total = f->total;
     PSGD_HIP(launch_flat_pack(f->dtype, a, s));
     return PSGD_OK;
 }

@@ -7,6 +7,43 @@
 
 namespace psgd {
 
+// ---------------------------------------------------------------- wave reductions
+// All-reduce of one float over the 64 lanes: 4 DPP row rotations (within rows of 16 lanes),
+// then the gfx950 half-exchanges v_permlane16_swap / v_permlane32_swap. No LDS traffic.
+__device__ __forceinline__ float wave_allsum(float v) {
+    v += dpp<0x128>(v);  // row_ror:8
+    v += dpp<0x124>(v);  // row_ror:4
+    v += dpp<0x122>(v);  // row_ror:2
+    v += dpp<0x121>(v);  // row_ror:1
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// Sum NV floats over a workgroup of NW waves; result in every thread. `red` holds
+// 2 * NW * NV floats (double-buffered by `phase`, so one barrier per call suffices).
+template <int NV, int NW>
+__device__ __forceinline__ void wg_sum(float (&v)[NV], float* red, int& phase) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_allsum(v[i]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float* buf = red + phase * NW * NV;
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) buf[wave * NV + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        float s = buf[i];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s += buf[w * NV + i];
+        v[i] = s;
+    }
+    phase ^= 1;
+}
+
 // ---------------------------------------------------------------- block reductions
 template <typename A, int NV>
 __device__ __forceinline__ void block_sum(A (&v)[NV], A* red) {
@@ -162,6 +199,220 @@ __global__ __launch_bounds__(kBlock) void k_orth(OrthArgs a, int64_t lds_floats)
     }
 }
 
+// ----------------------------------------------------------- fast orthonormalise
+constexpr int kOrthThreads = 1024;
+constexpr int kOrthWaves = kOrthThreads / 64;
+
+// rank 1: x /= max(||x||, 1e-16) over the whole shape group (two streaming passes, the
+// second one from L2). Optionally saves the pre-normalisation values.
+__device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red) {
+    float* __restrict__ st = a.state + u.off;
+    float* __restrict__ hx = a.hx + u.off;
+    float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+    const int64_t total = u.k * u.count;
+    const int tid = threadIdx.x;
+    constexpr int U = 8;
+    float part = 0.f;
+    for (int64_t base = tid; base < total; base += int64_t(U) * kOrthThreads) {
+        float x[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t i = base + int64_t(q) * kOrthThreads;
+            x[q] = i < total ? st[i] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) part = fmaf(x[q], x[q], part);
+    }
+    // block sum in double (wave partials in fp32 are exact enough: <= 64 * U terms each)
+    double s = wave_allsum(part);
+    double* rd = reinterpret_cast<double*>(red);
+    if ((tid & 63) == 0) rd[tid >> 6] = s;
+    __syncthreads();
+    s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kOrthWaves; ++w) s += rd[w];
+    const float nrm = float(sqrt(s));
+    const float d = nrm > 1e-16f ? nrm : 1e-16f;  // torch.maximum(norm, eps)
+    for (int64_t base = tid; base < total; base += int64_t(U) * kOrthThreads) {
+        float x[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t i = base + int64_t(q) * kOrthThreads;
+            x[q] = i < total ? st[i] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t i = base + int64_t(q) * kOrthThreads;
+            if (i < total) {
+                if (sv) sv[i] = x[q];
+                const float y = x[q] / d;
+                st[i] = y;
+                hx[i] = y;
+            }
+        }
+    }
+}
+
+// rank > 1: the k x r panel lives in registers (thread t owns rows t + 1024 q, q < RPT);
+// LAPACK geqr2 + org2r as 3r - 1 workgroup reductions.
+template <int R, int RPT>
+__global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
+    __shared__ __attribute__((aligned(16))) float red[2 * kOrthWaves * (R > 2 ? R : 2)];
+    const OrthUnit u = a.units[blockIdx.x];
+    if (u.r == 1) {
+        orth_joint_norm(a, u, red);
+        return;
+    }
+    if constexpr (R > 1) {
+        const int r = u.r;
+        const int64_t k = u.k;
+        const int tid = threadIdx.x;
+        float* __restrict__ st = a.state + u.off;
+        float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+        float A[RPT][R];
+        // every load first (all in flight together), then the save-copy stores
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int64_t i = tid + int64_t(q) * kOrthThreads;
+#pragma unroll
+            for (int c = 0; c < R; ++c) A[q][c] = (i < k && c < r) ? st[i * r + c] : 0.f;
+        }
+        if (sv) {
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int64_t i = tid + int64_t(q) * kOrthThreads;
+                if (i < k) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c)
+                        if (c < r) sv[i * r + c] = A[q][c];
+                }
+            }
+        }
+        int phase = 0;
+        float tau[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            tau[j] = 0.f;
+            if (j >= r) continue;
+            float v2[2] = {0.f, 0.f};  // sum_{i>j} A[i][j]^2, alpha = A[j][j]
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int64_t i = tid + int64_t(q) * kOrthThreads;
+                const float x = A[q][j];
+                if (i > j && i < k) v2[0] = fmaf(x, x, v2[0]);
+                if (i == j) v2[1] = x;
+            }
+            wg_sum<2, kOrthWaves>(v2, red, phase);
+            const float alpha = v2[1];
+            float tj = 0.f;
+            if (v2[0] != 0.f) {
+                const float beta = -copysignf(hypotf(alpha, sqrtf(v2[0])), alpha);
+                tj = (beta - alpha) / beta;
+                const float scal = 1.f / (alpha - beta);
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    const int64_t i = tid + int64_t(q) * kOrthThreads;
+                    if (i > j && i < k) A[q][j] *= scal;
+                    if (i == j) A[q][j] = beta;
+                }
+            }
+            tau[j] = tj;
+            if (tj != 0.f && j + 1 < r) {  // apply H_j to A[j:, j+1:]
+                float w[R];
+#pragma unroll
+                for (int c = 0; c < R; ++c) w[c] = 0.f;
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    const int64_t i = tid + int64_t(q) * kOrthThreads;
+                    const float vi = i == j ? 1.f : ((i > j && i < k) ? A[q][j] : 0.f);
+#pragma unroll
+                    for (int c = j + 1; c < R; ++c) w[c] = fmaf(vi, A[q][c], w[c]);
+                }
+                wg_sum<R, kOrthWaves>(w, red, phase);
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    const int64_t i = tid + int64_t(q) * kOrthThreads;
+                    const float vi = i == j ? 1.f : ((i > j && i < k) ? A[q][j] : 0.f);
+#pragma unroll
+                    for (int c = j + 1; c < R; ++c) A[q][c] -= tj * vi * w[c];
+                }
+            }
+        }
+        // org2r: Q = H_0 ... H_{r-1} I[:, :r]
+#pragma unroll
+        for (int j = R - 1; j >= 0; --j) {
+            if (j >= r) continue;
+            const float tj = tau[j];
+            if (j + 1 < r && tj != 0.f) {
+                float w[R];
+#pragma unroll
+                for (int c = 0; c < R; ++c) w[c] = 0.f;
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    const int64_t i = tid + int64_t(q) * kOrthThreads;
+                    const float vi = i == j ? 1.f : ((i > j && i < k) ? A[q][j] : 0.f);
+#pragma unroll
+                    for (int c = j + 1; c < R; ++c) w[c] = fmaf(vi, A[q][c], w[c]);
+                }
+                wg_sum<R, kOrthWaves>(w, red, phase);
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) {
+                    const int64_t i = tid + int64_t(q) * kOrthThreads;
+                    const float vi = i == j ? 1.f : ((i > j && i < k) ? A[q][j] : 0.f);
+#pragma unroll
+                    for (int c = j + 1; c < R; ++c) A[q][c] -= tj * vi * w[c];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int64_t i = tid + int64_t(q) * kOrthThreads;
+                if (i > j && i < k) A[q][j] *= -tj;
+                else if (i == j) A[q][j] = 1.f - tj;
+                else if (i < j) A[q][j] = 0.f;
+            }
+        }
+        float* __restrict__ hx = a.hx + u.off;
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int64_t i = tid + int64_t(q) * kOrthThreads;
+            if (i < k) {
+#pragma unroll
+                for (int c = 0; c < R; ++c)
+                    if (c < r) {
+                        st[i * r + c] = A[q][c];
+                        hx[i * r + c] = A[q][c];
+                    }
+            }
+        }
+    }
+}
+
+// Register budget: 1024-thread workgroups get at most 128 VGPRs, so the panel slice a
+// thread holds is capped at kOrthRegFloats floats (no spills for any instantiated pair).
+// (checked with -Rpass-analysis=kernel-resource-usage: ranks 16/32 spill, so they take the
+// LDS kernel above).
+__host__ __device__ constexpr bool orth_reg_ok(int R, int RPT) {
+    return R == 1 || (R <= 4 && R * RPT <= 32) || (R == 8 && RPT <= 2);
+}
+
+template <int R, int RPT>
+void launch_orth_reg_one(const OrthArgs& a, int nunits, hipStream_t s) {
+    if constexpr (orth_reg_ok(R, RPT)) k_orth_reg<R, RPT><<<nunits, kOrthThreads, 0, s>>>(a);
+}
+
+template <int R>
+hipError_t launch_orth_reg_r(int rpt, const OrthArgs& a, int nunits, hipStream_t s) {
+    switch (rpt) {
+        case 1: launch_orth_reg_one<R, 1>(a, nunits, s); break;
+        case 2: launch_orth_reg_one<R, 2>(a, nunits, s); break;
+        case 4: launch_orth_reg_one<R, 4>(a, nunits, s); break;
+        case 8: launch_orth_reg_one<R, 8>(a, nunits, s); break;
+        case 16: launch_orth_reg_one<R, 16>(a, nunits, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_orth_r(int R, const OrthArgs& a, int nunits, int64_t lds_floats, hipStream_t s) {
     const size_t bytes = size_t(lds_floats) * sizeof(float);
     switch (R) {
@@ -176,9 +427,22 @@ hipError_t launch_orth_r(int R, const OrthArgs& a, int nunits, int64_t lds_float
     return hipGetLastError();
 }
 
-hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t panel, hipStream_t s) {
+hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
+    // register-resident path when the longest rank>1 panel fits RPT * R <= 128 floats/thread
+    int64_t rpt = 1;
+    while (rpt * kOrthThreads < kmax) rpt <<= 1;
+    if (R == 1) return launch_orth_reg_r<1>(1, a, nunits, s);
+    if (rpt <= 16 && orth_reg_ok(R, int(rpt))) {
+        switch (R) {
+            case 2: return launch_orth_reg_r<2>(int(rpt), a, nunits, s);
+            case 4: return launch_orth_reg_r<4>(int(rpt), a, nunits, s);
+            case 8: return launch_orth_reg_r<8>(int(rpt), a, nunits, s);
+            default: break;
+        }
+    }
     constexpr int64_t kLdsCap = 60 * 1024 / 4;  // dynamic LDS floats (stays under the 64 KiB default)
-    const int64_t lds = R > 1 ? (panel < kLdsCap ? panel : kLdsCap) : 0;
+    const int64_t panel = kmax * R;
+    const int64_t lds = panel < kLdsCap ? panel : kLdsCap;
     return launch_orth_r(R, a, nunits, lds, s);
 }
 
@@ -191,19 +455,20 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     const int64_t len = (a.even ? d.m : d.n) * d.r;
     const int64_t e = int64_t(it.start) + threadIdx.x;
     if (e >= len) return;
-    float s;
-    int64_t dst;
-    if (a.even) {
-        const float* p = a.part + d.part_even + e;
-        s = p[0];
-        for (int c = 1; c < d.nchunk; ++c) s += p[int64_t(c) * len];
-        dst = d.qoff + e;
-    } else {
-        const float* p = a.part + d.part_odd + e;
-        s = p[0];
-        for (int c = 1; c < d.nstrip; ++c) s += p[int64_t(c) * len];
-        dst = d.poff + e;
+    const float* p = a.part + (a.even ? d.part_even : d.part_odd) + e;
+    const int np = a.even ? d.nchunk : d.odd_nstrip;
+    const int64_t dst = (a.even ? d.qoff : d.poff) + e;
+    // fixed summation order c = 0, 1, ..., np-1; loads issued 8 at a time
+    float s = p[0];
+    int c = 1;
+    for (; c + 8 <= np; c += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q) * len];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += v[q];
     }
+    for (; c < np; ++c) s += p[int64_t(c) * len];
     a.yloc[dst] = s;
     a.state[dst] = s;
 }
@@ -218,38 +483,37 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
 // then x = 0. One read + two writes per element.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_flat_pack(FlatArgs a) {
-    const int64_t chunk = int64_t(blockIdx.x) * kBlock * 4;
-    const FlatEntry* ents = a.entries;
-    // entry lookup: binary search on dense offsets (count is small)
-    int lo = 0, hi = a.count - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (ents[mid].off <= chunk) lo = mid; else hi = mid - 1;
-    }
+    const FlatItem it = a.items[blockIdx.x];
+    const FlatEntry en = a.entries[it.entry];
+    const gptr<T> x = gmut<T>(a.tensors[en.tensor]);
+    const gptr<T> f = gmut<T>(a.flat) + en.off;
     const float w = float(a.world);
-    for (int q = 0; q < 4; ++q) {
-        const int64_t e = chunk + int64_t(q) * kBlock + threadIdx.x;
-        if (e >= a.total) return;
-        int i = lo;
-        while (i + 1 < a.count && ents[i + 1].off <= e) ++i;
-        T* x = static_cast<T*>(a.tensors[ents[i].tensor]);
-        const int64_t j = e - ents[i].off;
-        float v[1];
-        Io<T>::ld(x + j, v);
-        if (a.world != 1) v[0] = v[0] / w;
-        Io<T>::st(static_cast<T*>(a.flat) + e, v);
-        const float z[1] = {0.f};
-        Io<T>::st(x + j, z);
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int64_t j = it.start + int64_t(q) * kBlock + threadIdx.x;
+        float t[1];
+        Io<T>::ld(x + (j < en.numel ? j : 0), t);  // clamped, unconditional
+        v[q] = t[0];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int64_t j = it.start + int64_t(q) * kBlock + threadIdx.x;
+        if (j < en.numel) {
+            float t[1] = {a.world != 1 ? v[q] / w : v[q]};
+            Io<T>::st(f + j, t);
+            const float z[1] = {0.f};
+            Io<T>::st(x + j, z);
+        }
     }
 }
 
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s) {
-    if (a.total == 0) return hipSuccess;
-    const int64_t blocks = (a.total + kBlock * 4 - 1) / (kBlock * 4);
+    if (a.nitems == 0) return hipSuccess;
     if (dtype == 0)
-        k_flat_pack<float><<<dim3(unsigned(blocks)), kBlock, 0, s>>>(a);
+        k_flat_pack<float><<<a.nitems, kBlock, 0, s>>>(a);
     else
-        k_flat_pack<bf16_t><<<dim3(unsigned(blocks)), kBlock, 0, s>>>(a);
+        k_flat_pack<bf16_t><<<a.nitems, kBlock, 0, s>>>(a);
     return hipGetLastError();
 }
 

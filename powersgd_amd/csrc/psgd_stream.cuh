@@ -1,31 +1,29 @@
 // Streaming kernels of the PowerSGD hot path, written for CDNA4 (gfx950, wave64).
 //
-// All three kernels walk the same tiles: a tile is (matrix, column strip, row chunk).
-// Inside a 256-thread workgroup every lane OWNS a fixed group of V consecutive columns
-// (V = 4 -> 16-byte fp32 / 8-byte bf16 vector loads) and the workgroup's 4 waves x RW row
-// phases walk the chunk's rows. Rows are contiguous in HBM, so every wave-instruction
-// reads L*V*sizeof(T) contiguous bytes per row (L = lanes per row, up to 64 -> 1 KiB).
-// Per-column factor values (Q-layout panels, [m, r]) are kept in registers for the whole
-// tile; per-row factor values (P-layout panels, [n, r]) are broadcast loads (one address
-// per row group, L1-resident).
+// k_product<EVEN=true> and k_apply walk lane-column tiles: a tile is (matrix, column strip,
+// row chunk) and inside a 256-thread workgroup every lane OWNS V consecutive columns
+// (V = 4 -> 16-byte fp32 / 8-byte bf16 vector loads) while the 4 waves x RW row phases walk
+// the chunk's rows. A wave-instruction reads L*V*sizeof(T) contiguous bytes of one row
+// (L = lanes per row, up to 64 -> 1 KiB). Q-layout factor values ([m, r], per column) stay
+// in registers for the whole tile; P-layout values ([n, r], per row) are broadcast loads.
 //
-//   k_product<EVEN>  reference powersgd.py:185-202
-//     even: Y[j,:] = sum_i Gk[i,j] X[i,:]   (Q = Gk^T P)   -> per-lane column accumulators,
-//           reduced over the workgroup's row phases in LDS -> one partial per row chunk.
-//     odd:  Y[i,:] = sum_j Gk[i,j] X[j,:]   (P = Gk Q)     -> per-row dot, reduced across
-//           the L lanes of the row -> one partial per column strip.
-//     Gk = G0 - sum_{j<k} P_j Q_j^T is formed ON THE FLY from the untouched gradient
-//     (same per-element arithmetic as the reference's baddbmm_, :195-202), so the
-//     iteration reads the gradient once and writes nothing back.
-//   k_apply          reference powersgd.py:195-230 (all iterations at once)
-//     residual = G0 - sum_k P_k Q_k^T (local factors)  -> written over the gradient
-//     output   = sum_k alpha * P_k Qbar_k^T            -> written to the flat output
-//     One read + two writes per element: the only pass that writes the gradient matrix.
+//   k_product<EVEN>   reference powersgd.py:185-202
+//     even: Q = Gk^T P -> per-lane column accumulators, reduced over the workgroup's row
+//           phases (DPP + LDS) into one partial per row chunk.
+//     odd:  P = Gk Q   -> k_odd_mfma (matrix cores, below); the lane-column VALU variant is
+//           kept for matrices without the 16-byte vector layout.
+//     Gk = G0 - sum_{j<k} P_j Q_j^T is formed ON THE FLY from the untouched gradient (the
+//     reference's baddbmm_, :195-202, element by element), so an iteration reads the
+//     gradient once and writes nothing back.
+//   k_apply           reference powersgd.py:195-230, all iterations at once:
+//     residual = G0 - sum_k P_k Q_k^T (local factors)  -> written over the gradient,
+//     output   = sum_k alpha P_k Qbar_k^T              -> written to the flat output.
+//     One read + two writes per element: the only pass that writes matrix-sized data.
 //
-// Template parameters: T = storage type (float / bf16 bits), R = rank bucket (runtime
-// r <= R; c >= r lanes hold zeros), K/NI = number of terms (-1: runtime count, Q-layout
-// panels re-read from L1 instead of cached in registers), V = vector width (runtime branch
-// per matrix, wave-uniform).
+// Codegen rules applied throughout (see cdna_hip_programming.md): every global pointer is
+// cast to address space 1 (global_load/store, not flat_*); loads are unconditional from
+// clamped in-range addresses and masked with selects afterwards (no exec-mask branch per
+// load); cross-lane sums use DPP row rotations and the gfx950 permlane16/32 swaps.
 #pragma once
 
 #include <hip/hip_bf16.h>
@@ -35,11 +33,27 @@
 
 namespace psgd {
 
+#define PSGD_G __attribute__((address_space(1)))
+template <typename T>
+using gptr = PSGD_G T*;
+
+template <typename T>
+__device__ __forceinline__ gptr<const T> gconst(const void* p) {
+    return (gptr<const T>)(static_cast<const T*>(p));
+}
+template <typename T>
+__device__ __forceinline__ gptr<T> gmut(void* p) {
+    return (gptr<T>)(static_cast<T*>(p));
+}
+
 using bf16_t = uint16_t;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) {
-    return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN preserving
+    return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN preserving (v_cvt_pk_bf16_f32)
 }
 
 template <typename T>
@@ -47,62 +61,70 @@ struct Io;
 
 template <>
 struct Io<float> {
-    static __device__ __forceinline__ void ld(const float* p, float (&v)[4]) {
-        const float4 x = *reinterpret_cast<const float4*>(p);
+    static __device__ __forceinline__ void ld(gptr<const float> p, float (&v)[4]) {
+        const v4f x = *(gptr<const v4f>)p;
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
     }
-    static __device__ __forceinline__ void ld(const float* p, float (&v)[1]) { v[0] = *p; }
-    static __device__ __forceinline__ void st(float* p, const float (&v)[4]) {
-        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    static __device__ __forceinline__ void ld(gptr<const float> p, float (&v)[1]) { v[0] = *p; }
+    static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[4]) {
+        const v4f x = {v[0], v[1], v[2], v[3]};
+        *(gptr<v4f>)p = x;
     }
-    static __device__ __forceinline__ void st(float* p, const float (&v)[1]) { *p = v[0]; }
+    static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[1]) { *p = v[0]; }
 };
 
 template <>
 struct Io<bf16_t> {
-    static __device__ __forceinline__ void ld(const bf16_t* p, float (&v)[4]) {
-        const uint2 x = *reinterpret_cast<const uint2*>(p);
+    static __device__ __forceinline__ void ld(gptr<const bf16_t> p, float (&v)[4]) {
+        const v2u x = *(gptr<const v2u>)p;
         v[0] = __uint_as_float(x.x << 16);
         v[1] = __uint_as_float(x.x & 0xffff0000u);
         v[2] = __uint_as_float(x.y << 16);
         v[3] = __uint_as_float(x.y & 0xffff0000u);
     }
-    static __device__ __forceinline__ void ld(const bf16_t* p, float (&v)[1]) { v[0] = bf2f(*p); }
-    static __device__ __forceinline__ void st(bf16_t* p, const float (&v)[4]) {
-        uint2 x;
+    static __device__ __forceinline__ void ld(gptr<const bf16_t> p, float (&v)[1]) { v[0] = bf2f(*p); }
+    static __device__ __forceinline__ void st(gptr<bf16_t> p, const float (&v)[4]) {
+        v2u x;
         x.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
         x.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-        *reinterpret_cast<uint2*>(p) = x;
+        *(gptr<v2u>)p = x;
     }
-    static __device__ __forceinline__ void st(bf16_t* p, const float (&v)[1]) { *p = f2bf(v[0]); }
+    static __device__ __forceinline__ void st(gptr<bf16_t> p, const float (&v)[1]) { *p = f2bf(v[0]); }
 };
 
-// r (<= R) consecutive fp32 factor values; zeros for c >= r. When r == R the row start is
-// R-aligned (every panel offset is a multiple of r), so R in {2,4,8,...} uses vector loads.
+// r (<= R) consecutive fp32 factor values, zeros for c >= r. When r == R the row start is
+// R-aligned (every panel offset is a multiple of r): vector loads for R in {2, 4, 8}.
 template <int R>
-__device__ __forceinline__ void ld_factor(const float* __restrict__ p, int r, float (&v)[R]) {
-    if (r == R) {
-        if constexpr (R % 4 == 0) {
+__device__ __forceinline__ void ld_factor(gptr<const float> p, int r, float (&v)[R]) {
+    if constexpr (R == 1) {
+        v[0] = p[0];
+    } else {
+        if (r == R) {
+            if constexpr (R % 4 == 0) {
 #pragma unroll
-            for (int c = 0; c < R; c += 4) {
-                const float4 x = *reinterpret_cast<const float4*>(p + c);
-                v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
+                for (int c = 0; c < R; c += 4) {
+                    const v4f x = *(gptr<const v4f>)(p + c);
+                    v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
+                }
+            } else if constexpr (R == 2) {
+                const v2f x = *(gptr<const v2f>)p;
+                v[0] = x.x; v[1] = x.y;
+            } else {
+#pragma unroll
+                for (int c = 0; c < R; ++c) v[c] = p[c];
             }
-        } else if constexpr (R == 2) {
-            const float2 x = *reinterpret_cast<const float2*>(p);
-            v[0] = x.x; v[1] = x.y;
         } else {
 #pragma unroll
-            for (int c = 0; c < R; ++c) v[c] = p[c];
+            for (int c = 0; c < R; ++c) {
+                const float x = p[c < r ? c : 0];
+                v[c] = c < r ? x : 0.f;
+            }
         }
-    } else {
-#pragma unroll
-        for (int c = 0; c < R; ++c) v[c] = c < r ? p[c] : 0.f;
     }
 }
 
-// sum_c a[c] * b[c] as an fma chain in c order (the order of a rank-r dot in the
-// reference's batched GEMM for one output element).
+// sum_c a[c] * b[c] as an fma chain in c order (the order of a rank-r dot of one output
+// element in the reference's batched GEMM).
 template <int R>
 __device__ __forceinline__ float dotr(const float (&a)[R], const float (&b)[R]) {
     float t = a[0] * b[0];
@@ -111,9 +133,50 @@ __device__ __forceinline__ float dotr(const float (&a)[R], const float (&b)[R]) 
     return t;
 }
 
+// ------------------------------------------------------------ cross-lane sums -------
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// Coset all-reduce steps: v + v(partner at distance s). Rotations within 16-lane rows
+// (row_ror) are equivalent to xor-partners once applied for every power of two up to 8;
+// s = 16 / 32 use the gfx950 half-exchanges. `on` is wave-uniform: a disabled step is a
+// select, not a branch, so independent sums interleave freely.
+__device__ __forceinline__ float swap16_sum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float swap32_sum(float v) {
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// sum over the lanes that share lane / L (partners lane ^ s, s < L); L = 1..64, power of 2
+__device__ __forceinline__ float sum_within(float v, int L) {
+    float t;
+    t = v + dpp<0x121>(v); v = L > 1 ? t : v;
+    t = v + dpp<0x122>(v); v = L > 2 ? t : v;
+    t = v + dpp<0x124>(v); v = L > 4 ? t : v;
+    t = v + dpp<0x128>(v); v = L > 8 ? t : v;
+    t = swap16_sum(v);     v = L > 16 ? t : v;
+    t = swap32_sum(v);     v = L > 32 ? t : v;
+    return v;
+}
+// sum over the lanes that share lane % L (partners lane ^ s, L <= s < 64)
+__device__ __forceinline__ float sum_across(float v, int L) {
+    float t;
+    t = v + dpp<0x121>(v); v = L <= 1 ? t : v;
+    t = v + dpp<0x122>(v); v = L <= 2 ? t : v;
+    t = v + dpp<0x124>(v); v = L <= 4 ? t : v;
+    t = v + dpp<0x128>(v); v = L <= 8 ? t : v;
+    t = swap16_sum(v);     v = L <= 16 ? t : v;
+    t = swap32_sum(v);     v = L <= 32 ? t : v;
+    return v;
+}
+
 struct TileGeom {
     int lane, wave, L, sub, ql;
-    int64_t n, m, col0, row_begin, row_end, first_row;
+    int64_t n, m, row_begin, row_end, first_row;
+    int32_t col0, ccol;  // this lane's first column; clamped copy that is always in range
     int stride;
     bool active;
 };
@@ -129,8 +192,9 @@ __device__ __forceinline__ TileGeom tile_geom(const MatDesc& d, const Tile& t) {
     g.ql = g.lane - g.sub * g.L;
     g.n = d.n;
     g.m = d.m;
-    g.col0 = (int64_t(t.strip) * g.L + g.ql) * V;
+    g.col0 = (t.strip * g.L + g.ql) * V;
     g.active = g.col0 < g.m;  // V == 4 only when m % 4 == 0: the whole vector is in range
+    g.ccol = g.active ? g.col0 : 0;
     g.row_begin = int64_t(t.chunk) * d.chunk_rows;
     g.row_end = g.n < g.row_begin + d.chunk_rows ? g.n : g.row_begin + d.chunk_rows;
     g.stride = kWaves * rw;
@@ -146,23 +210,24 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                                              float* lds) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
-    const T* __restrict__ G = static_cast<const T*>(a.grads[d.tensor]);
+    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
     const int nres = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;  // register-cached terms
+    const gptr<const float> xp_base = gconst<float>(a.x) + d.poff;
+    const gptr<const float> xq_base = gconst<float>(a.x) + d.qoff;
 
-    // Q-layout values at this lane's columns (clamped to a valid column when inactive).
-    const int64_t ccol = g.active ? g.col0 : 0;
     float bq[KC][V][R];
     if constexpr (K > 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-            for (int v = 0; v < V; ++v) ld_factor<R>(a.res.q[k] + d.qoff + (ccol + v) * r, r, bq[k][v]);
+            for (int v = 0; v < V; ++v)
+                ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bq[k][v]);
     }
     float xq[EVEN ? 1 : V][R];
     if constexpr (!EVEN) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) ld_factor<R>(a.x + d.qoff + (ccol + v) * r, r, xq[v]);
+        for (int v = 0; v < V; ++v) ld_factor<R>(xq_base + (g.ccol + v) * r, r, xq[v]);
     }
     float acc[EVEN ? V : 1][R];
 #pragma unroll
@@ -172,25 +237,21 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 
     for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
         float x[kUnroll][V];
+        int64_t rc[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
-            if (g.active && rr < g.row_end) {
-                Io<T>::ld(G + rr * g.m + g.col0, x[u]);
-            } else {
-#pragma unroll
-                for (int v = 0; v < V; ++v) x[u][v] = 0.f;
-            }
+            rc[u] = rr < g.row_end ? rr : g.row_begin;  // clamped: every load is in range
+            Io<T>::ld(G + rc[u] * g.m + g.ccol, x[u]);
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t rr = row + u * g.stride;
-            const bool valid = g.active && rr < g.row_end;
-            const int64_t rc = rr < g.row_end ? rr : g.row_begin;  // clamped for factor loads
+            const bool valid = g.active && (row + u * g.stride) < g.row_end;
+            const int32_t prow = int32_t(rc[u]) * r;
             // error feedback of the previous iterations, formed on the fly
             for (int k = 0; k < nres; ++k) {
                 float ap[R];
-                ld_factor<R>(a.res.p[k] + d.poff + rc * r, r, ap);
+                ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     float b[R];
@@ -198,18 +259,16 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 #pragma unroll
                         for (int c = 0; c < R; ++c) b[c] = bq[k < KC ? k : 0][v][c];
                     } else {
-                        ld_factor<R>(a.res.q[k] + d.qoff + (ccol + v) * r, r, b);
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, b);
                     }
                     x[u][v] = x[u][v] - dotr<R>(ap, b);
                 }
             }
-            if (!valid) {
 #pragma unroll
-                for (int v = 0; v < V; ++v) x[u][v] = 0.f;
-            }
+            for (int v = 0; v < V; ++v) x[u][v] = valid ? x[u][v] : 0.f;
             if constexpr (EVEN) {
                 float xp[R];
-                ld_factor<R>(a.x + d.poff + rc * r, r, xp);
+                ld_factor<R>(xp_base + prow, r, xp);
 #pragma unroll
                 for (int v = 0; v < V; ++v)
 #pragma unroll
@@ -221,14 +280,11 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                     float s = x[u][0] * xq[0][c];
 #pragma unroll
                     for (int v = 1; v < V; ++v) s = fmaf(x[u][v], xq[v][c], s);
-                    dot[c] = s;
+                    dot[c] = sum_within(s, g.L);
                 }
-                for (int s = g.L >> 1; s > 0; s >>= 1) {
-#pragma unroll
-                    for (int c = 0; c < R; ++c) dot[c] += __shfl_xor(dot[c], s);
-                }
+                const int64_t rr = row + u * g.stride;
                 if (g.ql == 0 && rr < g.row_end) {
-                    float* dst = a.part + d.part_odd + (int64_t(t.strip) * g.n + rr) * r;
+                    gptr<float> dst = gmut<float>(a.part) + d.part_odd + (int64_t(t.strip) * g.n + rr) * r;
 #pragma unroll
                     for (int c = 0; c < R; ++c)
                         if (c < r) dst[c] = dot[c];
@@ -238,13 +294,10 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
     }
 
     if constexpr (EVEN) {
-        // reduce the RW row phases inside the wave (lanes ql, ql+L, ...)
-        for (int s = g.L; s < 64; s <<= 1) {
 #pragma unroll
-            for (int v = 0; v < V; ++v)
+        for (int v = 0; v < V; ++v)
 #pragma unroll
-                for (int c = 0; c < R; ++c) acc[v][c] += __shfl_xor(acc[v][c], s);
-        }
+            for (int c = 0; c < R; ++c) acc[v][c] = sum_across(acc[v][c], g.L);  // row phases
         const int width = g.L * V * R;  // floats per wave
         if (g.sub == 0) {
 #pragma unroll
@@ -253,13 +306,14 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                 for (int c = 0; c < R; ++c) lds[g.wave * width + (g.ql * V + v) * R + c] = acc[v][c];
         }
         __syncthreads();
+        gptr<float> part = gmut<float>(a.part) + d.part_even + int64_t(t.chunk) * g.m * r;
         for (int idx = threadIdx.x; idx < width; idx += kBlock) {
             float s = lds[idx];
 #pragma unroll
             for (int w = 1; w < kWaves; ++w) s += lds[w * width + idx];
             const int c = idx % R;
             const int64_t col = int64_t(t.strip) * g.L * V + idx / R;
-            if (c < r && col < g.m) a.part[d.part_even + (int64_t(t.chunk) * g.m + col) * r + c] = s;
+            if (c < r && col < g.m) part[col * r + c] = s;
         }
     }
 }
@@ -279,17 +333,195 @@ __global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
     product_tile<T, R, K, EVEN, 1>(a, d, t, lds);
 }
 
+// ------------------------------------------------------- odd product on MFMA -------
+// P[i, c] = sum_j Gk[i, j] X[j, c] with v_mfma_f32_16x16x4_f32 (exact fp32 fma chains).
+// A wave owns 16 rows; lane l = (ri = l & 15, cq = l >> 4) loads G[i0+ri][j0+4cq .. +3]
+// (16 rows x 64 contiguous bytes per wave-instruction) and those four values are the
+// A-operands of four 16x16x4 products whose B-operand is X[j0+4cq+e][c = ri]: the matrix
+// core does the reduction over columns that a VALU version needs cross-lane sums for. The
+// error-feedback correction (A_t B_t^T)[i, j] of the same 16 x 16 sub-tile is one MFMA per
+// term and 4 factor columns, produced directly in the layout of the loaded fragment
+// (D[row=j][col=i] of B_t[16x4] . A_t^T[4x16]).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kOddSW = 256;            // max MFMA strip width (columns)
+constexpr int kOddXT = kOddSW + 4;      // padded row of the transposed X strip in LDS
+
+template <typename T, int RC, int K>
+__device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDesc& d, const Tile& t,
+                                              float* xt, float* bs) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ri = lane & 15, cq = lane >> 4;
+    const int r = d.r;
+    const int64_t n = d.n;
+    const int32_t m = int32_t(d.m);
+    const int32_t j_begin = t.strip * d.odd_sw;
+    const int32_t j_end = m < j_begin + d.odd_sw ? m : j_begin + d.odd_sw;
+    const int32_t sw = j_end - j_begin;
+    const int64_t row0 = int64_t(t.chunk) * d.odd_chunk_rows;
+    const int64_t row_end = n < row0 + d.odd_chunk_rows ? n : row0 + d.odd_chunk_rows;
+    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
+    const int nt = K >= 0 ? K : a.nres;
+    constexpr int KC = K > 0 ? K : 1;
+    constexpr int RP = 4 * RC;           // factor columns held per strip row in LDS
+    constexpr int U = 4;                 // k-steps (16 columns each) in flight per lane
+    const bool cvalid = ri < r;
+    const int cx = cvalid ? ri : 0;
+
+    // Stage the strip's factor panels once per tile: xt[c][j] = X[j_begin + j][c]
+    // (transposed: a lane's four B-operands of one k-step are one ds_read_b128) and
+    // bs[k][j][c] = B_k[j_begin + j][c] for the error-feedback correction.
+    {
+        const gptr<const float> X = gconst<float>(a.x) + d.qoff + int64_t(j_begin) * r;
+        for (int idx = threadIdx.x; idx < sw * r; idx += kBlock) {
+            const int j = idx / r, c = idx - j * r;
+            xt[c * kOddXT + j] = X[idx];
+        }
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const gptr<const float> Bq = gconst<float>(a.res.q[k]) + d.qoff + int64_t(j_begin) * r;
+                for (int idx = threadIdx.x; idx < sw * r; idx += kBlock) {
+                    const int j = idx / r, c = idx - j * r;
+                    bs[(k * kOddSW + j) * RP + c] = Bq[idx];
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    for (int64_t i0 = row0 + wave * 16; i0 < row_end; i0 += kWaves * 16) {
+        const int64_t i = i0 + ri;
+        const bool rv = i < row_end;
+        const int64_t ic = rv ? i : row0;
+        const gptr<const T> Grow = G + ic * m;
+        float at[KC][RC];
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+#pragma unroll
+            for (int b = 0; b < RC; ++b) at[k][b] = 0.f;
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int b = 0; b < RC; ++b) {
+                    const int c = cq + 4 * b;
+                    const float v = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
+                    at[k][b] = (rv && c < r) ? v : 0.f;
+                }
+        }
+        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+        for (int32_t j0 = 0; j0 < sw; j0 += 16 * U) {
+            float x[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t jj = j0 + 16 * u + 4 * cq;
+                Io<T>::ld(Grow + j_begin + (jj < sw ? jj : 0), x[u]);
+                const bool ok = rv && jj < sw;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[u][e] = ok ? x[u][e] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t js = j0 + 16 * u;
+                if (js >= sw) break;  // wave-uniform
+                if constexpr (K > 0) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int b = 0; b < RC; ++b) {
+                            const int c = cq + 4 * b;
+                            const int32_t jr = js + ri;
+                            const bool ok = jr < sw && c < r;
+                            const float av = bs[(k * kOddSW + (jr < sw ? jr : 0)) * RP + c];
+                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, at[k][b], corr, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[u][e] -= corr[e];
+                    }
+                } else {
+                    for (int k = 0; k < nt; ++k) {  // many terms: panels straight from L1/L2
+                        const gptr<const float> Bq = gconst<float>(a.res.q[k]) + d.qoff;
+                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int b = 0; b < RC; ++b) {
+                            const int c = cq + 4 * b;
+                            const int32_t jr = js + ri;
+                            const bool ok = jr < sw && c < r;
+                            const float av = Bq[int64_t(j_begin + (ok ? jr : 0)) * r + (ok ? c : 0)];
+                            const float pv = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
+                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, (rv && c < r) ? pv : 0.f,
+                                                                        corr, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[u][e] -= corr[e];
+                    }
+                }
+                const int32_t jq = js + 4 * cq;
+                const v4f bx4 = *reinterpret_cast<const v4f*>(xt + cx * kOddXT + (jq < sw ? jq : 0));
+                const bool okx = cvalid && jq < sw;  // sw % 4 == 0: the 4 columns are valid together
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][0], okx ? bx4.x : 0.f, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][1], okx ? bx4.y : 0.f, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][2], okx ? bx4.z : 0.f, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][3], okx ? bx4.w : 0.f, acc, 0, 0, 0);
+            }
+        }
+        // acc[e] = partial P[i0 + 4 cq + e][c = ri]
+        if (cvalid) {
+            gptr<float> part = gmut<float>(a.part) + d.part_odd + int64_t(t.strip) * n * r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t ii = i0 + 4 * cq + e;
+                if (ii < row_end) part[ii * r + ri] = acc[e];
+            }
+        }
+    }
+}
+
+template <typename T, int RC, int K>
+__global__ __launch_bounds__(kBlock) void k_odd_mfma(ProductArgs a) {
+    __shared__ __attribute__((aligned(16))) float xt[RC * 4 * kOddXT];
+    __shared__ __attribute__((aligned(16))) float bs[(K > 0 ? K : 1) * kOddSW * 4 * RC];
+    const Tile t = a.tiles[blockIdx.x];
+    const MatDesc d = a.mats[t.mat];
+    odd_mfma_tile<T, RC, K>(a, d, t, xt, bs);
+}
+
+template <typename T>
+hipError_t dispatch_odd_mfma(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+    const dim3 grid(ntiles), block(kBlock);
+    const int K = nres <= 3 ? nres : -1;
+#define PSGD_O(RC)                                                                       \
+    do {                                                                                 \
+        switch (K) {                                                                     \
+            case 0: k_odd_mfma<T, RC, 0><<<grid, block, 0, s>>>(a); break;               \
+            case 1: k_odd_mfma<T, RC, 1><<<grid, block, 0, s>>>(a); break;               \
+            case 2: k_odd_mfma<T, RC, 2><<<grid, block, 0, s>>>(a); break;               \
+            case 3: k_odd_mfma<T, RC, 3><<<grid, block, 0, s>>>(a); break;               \
+            default: k_odd_mfma<T, RC, -1><<<grid, block, 0, s>>>(a); break;             \
+        }                                                                                \
+    } while (0)
+    if (R <= 4)
+        PSGD_O(1);
+    else if (R <= 8)
+        PSGD_O(2);
+    else
+        return hipErrorInvalidValue;
+#undef PSGD_O
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ apply ---------
 template <typename T, int R, int NI, bool SHARED, int V>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
-    T* __restrict__ G = static_cast<T*>(a.grads[d.tensor]);
-    T* __restrict__ O = static_cast<T*>(a.out) + d.out_off;
+    const gptr<T> G = gmut<T>(a.grads[d.tensor]);
+    const gptr<T> O = gmut<T>(a.out) + d.out_off;
     const int nt = NI > 0 ? NI : a.nterms;
     constexpr int NC = NI > 0 ? NI : 1;
     constexpr int NA = (NI > 0 && !SHARED) ? NI : 1;
-    const int64_t ccol = g.active ? g.col0 : 0;
 
     float bq[NC][V][R];
     float ba[NA][V][R];
@@ -298,36 +530,33 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
         for (int k = 0; k < NI; ++k)
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                ld_factor<R>(a.res.q[k] + d.qoff + (ccol + v) * r, r, bq[k][v]);
-                if constexpr (!SHARED) ld_factor<R>(a.apx.q[k] + d.qoff + (ccol + v) * r, r, ba[k][v]);
+                ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bq[k][v]);
+                if constexpr (!SHARED)
+                    ld_factor<R>(gconst<float>(a.apx.q[k]) + d.qoff + (g.ccol + v) * r, r, ba[k][v]);
             }
     }
     const float alpha = a.alpha;
 
     for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
         float x[kUnroll][V];
+        int64_t rc[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
-            if (g.active && rr < g.row_end) {
-                Io<T>::ld(G + rr * g.m + g.col0, x[u]);
-            } else {
-#pragma unroll
-                for (int v = 0; v < V; ++v) x[u][v] = 0.f;
-            }
+            rc[u] = rr < g.row_end ? rr : g.row_begin;
+            Io<T>::ld(G + rc[u] * g.m + g.ccol, x[u]);
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t rr = row + u * g.stride;
-            const int64_t rc = rr < g.row_end ? rr : g.row_begin;
+            const int32_t prow = int32_t(rc[u]) * r;
             float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) o[v] = 0.f;
             for (int k = 0; k < nt; ++k) {
                 float ap[R];
-                ld_factor<R>(a.res.p[k] + d.poff + rc * r, r, ap);
+                ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
                 float aa[R];
-                if constexpr (!SHARED) ld_factor<R>(a.apx.p[k] + d.poff + rc * r, r, aa);
+                if constexpr (!SHARED) ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, aa);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     float b[R];
@@ -335,7 +564,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
 #pragma unroll
                         for (int c = 0; c < R; ++c) b[c] = bq[k < NC ? k : 0][v][c];
                     } else {
-                        ld_factor<R>(a.res.q[k] + d.qoff + (ccol + v) * r, r, b);
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, b);
                     }
                     const float tk = dotr<R>(ap, b);
                     x[u][v] = x[u][v] - tk;  // reference :195-202 (alpha = -1)
@@ -347,15 +576,15 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
 #pragma unroll
                             for (int c = 0; c < R; ++c) bb[c] = ba[k < NA ? k : 0][v][c];
                         } else {
-                            ld_factor<R>(a.apx.q[k] + d.qoff + (ccol + v) * r, r, bb);
+                            ld_factor<R>(gconst<float>(a.apx.q[k]) + d.qoff + (g.ccol + v) * r, r, bb);
                         }
                         o[v] = o[v] + alpha * dotr<R>(aa, bb);  // reference :211-219
                     }
                 }
             }
-            if (g.active && rr < g.row_end) {
-                Io<T>::st(G + rr * g.m + g.col0, x[u]);
-                Io<T>::st(O + rr * g.m + g.col0, o);
+            if (g.active && row + u * g.stride < g.row_end) {
+                Io<T>::st(G + rc[u] * g.m + g.col0, x[u]);
+                Io<T>::st(O + rc[u] * g.m + g.col0, o);
             }
         }
     }
