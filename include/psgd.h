@@ -118,6 +118,13 @@ int psgd_decompress(psgd_plan* plan, void* const* grads, void* out, int64_t step
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);
 
+/* Kernel timing for benchmarks: when enabled, every fused final pass (k_apply) launched by
+ * psgd_decompress/psgd_aggregate is bracketed by HIP events recorded on its own stream.
+ * psgd_plan_timing_read waits for the recorded events, returns the summed kernel time (ms)
+ * and the number of launches, and clears the record. */
+int psgd_plan_set_timing(psgd_plan* plan, int32_t enable);
+int psgd_plan_timing_read(psgd_plan* plan, double* total_ms, int32_t* launches);
+
 /* ------------------------------------------ uncompressed tensors: flat average ------ */
 /* AllReduce.aggregate minus the collective: flat[off_i + e] = x_i[e] / world_size (exact
  * copy when world_size == 1), then x_i[e] = 0. The caller SUM-all-reduces `flat` and

@@ -36,6 +36,8 @@ _SIGNATURES = {
     "psgd_compress": ([_vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_decompress": ([_vp, _vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_aggregate": ([_vp, _vp, _vp, _i64, _vp], _i32),
+    "psgd_plan_set_timing": ([_vp, _i32], _i32),
+    "psgd_plan_timing_read": ([_vp, _P_dbl, _P_i32], _i32),
     "psgd_flat_create": ([_P_i64, _i32, _i32, ctypes.POINTER(_vp)], _i32),
     "psgd_flat_destroy": ([_vp], _i32),
     "psgd_flat_workspace_bytes": ([_vp, _P_i64], _i32),
@@ -166,6 +168,15 @@ class Plan:
 
     def aggregate(self, grads, out_ptr: int, step: int, stream: int) -> None:
         check(lib().psgd_aggregate(self._h, grads, out_ptr, step, stream))
+
+    def set_timing(self, enable: bool) -> None:
+        check(lib().psgd_plan_set_timing(self._h, 1 if enable else 0))
+
+    def timing_read(self):
+        """(summed k_apply milliseconds, launches) since timing was enabled / last read."""
+        ms, n = _dbl(), _i32()
+        check(lib().psgd_plan_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
 
 
 class FlatPlan:

@@ -172,6 +172,17 @@ struct psgd_plan {
     float* Q = nullptr;
     char* ws = nullptr;
     std::vector<void*> host_ptrs;
+    // benchmark timing of k_apply: event pairs recorded on the launch stream
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    size_t ev_used = 0;
+
+    ~psgd_plan() {
+        for (auto& e : ev_pool) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+    }
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
         return reinterpret_cast<float*>(ws + o_hist) + (int64_t(which) * iters + k) * fmax;
@@ -608,7 +619,42 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     }
     aa.nterms = I;
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (p->timing) {
+        if (p->ev_used == p->ev_pool.size()) {
+            std::pair<hipEvent_t, hipEvent_t> e;
+            PSGD_HIP(hipEventCreate(&e.first));
+            PSGD_HIP(hipEventCreate(&e.second));
+            p->ev_pool.push_back(e);
+        }
+        ev = &p->ev_pool[p->ev_used++];
+        PSGD_HIP(hipEventRecord(ev->first, s));
+    }
     PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
+    if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
+    return PSGD_OK;
+}
+
+int psgd_plan_set_timing(psgd_plan* p, int32_t enable) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    p->timing = enable != 0;
+    p->ev_used = 0;
+    return PSGD_OK;
+}
+
+int psgd_plan_timing_read(psgd_plan* p, double* total_ms, int32_t* launches) {
+    if (!p || !total_ms || !launches) return fail(PSGD_ERR_VALUE, "null argument");
+    DevScope scope(p->device);
+    double sum = 0.0;
+    for (size_t i = 0; i < p->ev_used; ++i) {
+        PSGD_HIP(hipEventSynchronize(p->ev_pool[i].second));
+        float ms = 0.f;
+        PSGD_HIP(hipEventElapsedTime(&ms, p->ev_pool[i].first, p->ev_pool[i].second));
+        sum += ms;
+    }
+    *total_ms = sum;
+    *launches = int32_t(p->ev_used);
+    p->ev_used = 0;
     return PSGD_OK;
 }
 

@@ -232,7 +232,6 @@ class BasicPowerSGD(Aggregator):
         self._slab = _OutputSlab()
         self._ptr_key: Optional[tuple] = None
         self._ptr_arr = None
-        self._apply_events: Optional[list] = None  # set by bench.py to time k_apply
 
     def _grad_pointers(self, gradients: List[torch.Tensor]):
         key = tuple(g.data_ptr() for g in gradients)
@@ -259,23 +258,13 @@ class BasicPowerSGD(Aggregator):
         out_ptr = self._slab.flat.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
-        dist = is_distributed()
-        if dist or self._apply_events is not None:
-            world = torch.distributed.get_world_size() if dist else 1
+        if is_distributed():
+            world = torch.distributed.get_world_size()
             for it in range(self.config.num_iters_per_step):
                 self._plan.compress(ptrs, step, it, stream)
-                if dist:
-                    buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
-                    torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
-            if self._apply_events is not None:  # bench.py: time the fused final kernel on its stream
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                self._plan.decompress(ptrs, out_ptr, step, world, stream)
-                e1.record()
-                self._apply_events.append((e0, e1))
-            else:
-                self._plan.decompress(ptrs, out_ptr, step, world, stream)
+                buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
+                torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
+            self._plan.decompress(ptrs, out_ptr, step, world, stream)
         else:
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
