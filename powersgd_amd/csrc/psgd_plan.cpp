@@ -205,7 +205,7 @@ struct psgd_plan {
             d.nstrip = g.nstrip;
             d.nchunk = g.nchunk;
             d.chunk_rows = g.chunk_rows;
-            d.odd_mfma = (use_mfma && vec[i] && d.r <= 8) ? 1 : 0;
+            d.odd_mfma = (use_mfma && d.r <= 16) ? 1 : 0;
             for (int c = 0; c < g.nchunk; ++c)
                 for (int s = 0; s < g.nstrip; ++s) {
                     tiles.push_back(Tile{int32_t(i), s, c, 0});
@@ -329,7 +329,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->rank = rank;
     p->iters = iters;
     p->dtype = dtype;
-    p->tile_elems = std::max<int64_t>(1024, env_int("PSGD_TILE_ELEMS", 16384));
+    p->tile_elems = 0;  // set below from the compressed size
     std::map<std::pair<int64_t, int64_t>, int> gid;
     const int64_t* d = dims;
     for (int t = 0; t < num_tensors; ++t) {
@@ -371,6 +371,13 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     }
     int maxr = 1;
     for (auto& g : p->groups) maxr = std::max(maxr, g.r);
+    {
+        // about 1.5k tiles (6 per CU) on large problems, never below 4k elements per tile
+        int64_t total = 0;
+        for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
+        const int64_t dflt = std::min<int64_t>(16384, std::max<int64_t>(4096, total / 1536));
+        p->tile_elems = std::max<int64_t>(1024, env_int("PSGD_TILE_ELEMS", dflt));
+    }
     if (maxr > 32) {
         delete p;
         return fail(PSGD_ERR_VALUE, "effective rank above 32 is not supported by this build");
@@ -577,7 +584,7 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
         }
         if (!p->tiles_om.empty()) {
             pa.tiles = p->dev<Tile>(p->o_tiles_om);
-            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 8), it, pa, int(p->tiles_om.size()), s));
+            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), it, pa, int(p->tiles_om.size()), s));
         }
     }
 

@@ -216,9 +216,15 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red
     for (int64_t base = tid; base < total; base += int64_t(U) * kOrthThreads) {
         float x[U];
 #pragma unroll
+        for (int q = 0; q < U; ++q) {  // unconditional loads from clamped indices (no branches)
+            const int64_t i = base + int64_t(q) * kOrthThreads;
+            x[q] = st[i < total ? i : 0];
+        }
+#pragma unroll
         for (int q = 0; q < U; ++q) {
             const int64_t i = base + int64_t(q) * kOrthThreads;
-            x[q] = i < total ? st[i] : 0.f;
+            keep(x[q]);
+            x[q] = i < total ? x[q] : 0.f;
         }
 #pragma unroll
         for (int q = 0; q < U; ++q) part = fmaf(x[q], x[q], part);
@@ -238,8 +244,10 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red
 #pragma unroll
         for (int q = 0; q < U; ++q) {
             const int64_t i = base + int64_t(q) * kOrthThreads;
-            x[q] = i < total ? st[i] : 0.f;
+            x[q] = st[i < total ? i : 0];
         }
+#pragma unroll
+        for (int q = 0; q < U; ++q) keep(x[q]);
 #pragma unroll
         for (int q = 0; q < U; ++q) {
             const int64_t i = base + int64_t(q) * kOrthThreads;
@@ -272,10 +280,20 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
         float A[RPT][R];
         // every load first (all in flight together), then the save-copy stores
 #pragma unroll
+        for (int q = 0; q < RPT; ++q) {  // unconditional loads from clamped indices (no branches)
+            const int64_t i = tid + int64_t(q) * kOrthThreads;
+            const int64_t ic = i < k ? i : 0;
+#pragma unroll
+            for (int c = 0; c < R; ++c) A[q][c] = st[ic * r + (c < r ? c : 0)];
+        }
+#pragma unroll
         for (int q = 0; q < RPT; ++q) {
             const int64_t i = tid + int64_t(q) * kOrthThreads;
 #pragma unroll
-            for (int c = 0; c < R; ++c) A[q][c] = (i < k && c < r) ? st[i * r + c] : 0.f;
+            for (int c = 0; c < R; ++c) {
+                keep(A[q][c]);
+                A[q][c] = (i < k && c < r) ? A[q][c] : 0.f;
+            }
         }
         if (sv) {
 #pragma unroll
@@ -496,6 +514,8 @@ __global__ __launch_bounds__(kBlock) void k_flat_pack(FlatArgs a) {
         Io<T>::ld(x + (j < en.numel ? j : 0), t);  // clamped, unconditional
         v[q] = t[0];
     }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) keep(v[q]);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int64_t j = it.start + int64_t(q) * kBlock + threadIdx.x;

@@ -56,6 +56,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
     return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN preserving (v_cvt_pk_bf16_f32)
 }
 
+// Pin a loaded value: an empty asm that consumes it. Issued after a batch of loads, it stops
+// LLVM from sinking a load into the branch of the select that masks it (which costs an
+// exec-mask branch and a vmcnt(0) wait per load).
+__device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
+
 template <typename T>
 struct Io;
 
@@ -115,9 +120,11 @@ __device__ __forceinline__ void ld_factor(gptr<const float> p, int r, float (&v)
             }
         } else {
 #pragma unroll
+            for (int c = 0; c < R; ++c) v[c] = p[c < r ? c : 0];
+#pragma unroll
             for (int c = 0; c < R; ++c) {
-                const float x = p[c < r ? c : 0];
-                v[c] = c < r ? x : 0.f;
+                keep(v[c]);
+                v[c] = c < r ? v[c] : 0.f;
             }
         }
     }
@@ -347,7 +354,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kOddSW = 256;            // max MFMA strip width (columns)
 constexpr int kOddXT = kOddSW + 4;      // padded row of the transposed X strip in LDS
 
-template <typename T, int RC, int K>
+template <typename T, int VEC, int RC, int K>
 __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDesc& d, const Tile& t,
                                               float* xt, float* bs) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -376,6 +383,11 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
         for (int idx = threadIdx.x; idx < sw * r; idx += kBlock) {
             const int j = idx / r, c = idx - j * r;
             xt[c * kOddXT + j] = X[idx];
+        }
+        const int swp = (sw + 3) & ~3;
+        for (int idx = threadIdx.x; idx < (swp - sw) * r; idx += kBlock) {
+            const int j = sw + idx / r, c = idx % r;
+            xt[c * kOddXT + j] = 0.f;
         }
         if constexpr (K > 0) {
 #pragma unroll
@@ -416,10 +428,25 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int32_t jj = j0 + 16 * u + 4 * cq;
-                Io<T>::ld(Grow + j_begin + (jj < sw ? jj : 0), x[u]);
-                const bool ok = rv && jj < sw;
+                if constexpr (VEC) {  // sw % 4 == 0: the four columns are valid together
+                    Io<T>::ld(Grow + j_begin + (jj < sw ? jj : 0), x[u]);
+                } else {              // any m: four element loads, each clamped
 #pragma unroll
-                for (int e = 0; e < 4; ++e) x[u][e] = ok ? x[u][e] : 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        float v1[1];
+                        Io<T>::ld(Grow + j_begin + (jj + e < sw ? jj + e : 0), v1);
+                        x[u][e] = v1[0];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t jj = j0 + 16 * u + 4 * cq;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    keep(x[u][e]);
+                    x[u][e] = (rv && jj + (VEC ? 0 : e) < sw) ? x[u][e] : 0.f;
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -459,8 +486,9 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
                     }
                 }
                 const int32_t jq = js + 4 * cq;
+                // xt rows are zero-padded to a multiple of 4 columns: one aligned 16-byte read
                 const v4f bx4 = *reinterpret_cast<const v4f*>(xt + cx * kOddXT + (jq < sw ? jq : 0));
-                const bool okx = cvalid && jq < sw;  // sw % 4 == 0: the 4 columns are valid together
+                const bool okx = cvalid && jq < sw;
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][0], okx ? bx4.x : 0.f, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][1], okx ? bx4.y : 0.f, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][2], okx ? bx4.z : 0.f, acc, 0, 0, 0);
@@ -485,7 +513,10 @@ __global__ __launch_bounds__(kBlock) void k_odd_mfma(ProductArgs a) {
     __shared__ __attribute__((aligned(16))) float bs[(K > 0 ? K : 1) * kOddSW * 4 * RC];
     const Tile t = a.tiles[blockIdx.x];
     const MatDesc d = a.mats[t.mat];
-    odd_mfma_tile<T, RC, K>(a, d, t, xt, bs);
+    if (d.vec)
+        odd_mfma_tile<T, 1, RC, K>(a, d, t, xt, bs);
+    else
+        odd_mfma_tile<T, 0, RC, K>(a, d, t, xt, bs);
 }
 
 template <typename T>
@@ -506,6 +537,8 @@ hipError_t dispatch_odd_mfma(int R, int nres, const ProductArgs& a, int ntiles, 
         PSGD_O(1);
     else if (R <= 8)
         PSGD_O(2);
+    else if (R <= 16)
+        PSGD_O(4);
     else
         return hipErrorInvalidValue;
 #undef PSGD_O
