@@ -2,10 +2,30 @@
 // product partials, and the flat pack of uncompressed tensors.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "psgd_internal.h"
 #include "psgd_stream.cuh"
 
 namespace psgd {
+
+// Diagnostic-only phase stamps (tools/orth_stamps.hip builds this file with PSGD_STAMPS;
+// the library build never executes a stamp).
+#ifdef PSGD_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define PSGD_STAMP(i)                                                                         \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        unsigned long long t_;                                                                \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        if (threadIdx.x == 0 && blockIdx.x == 0) g_stamps[i] = t_;                            \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+#else
+#define PSGD_STAMP(i) \
+    do {              \
+    } while (0)
+#endif
 
 // ---------------------------------------------------------------- wave reductions
 // All-reduce of one float over the 64 lanes: 4 DPP row rotations (within rows of 16 lanes),
@@ -272,6 +292,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
         return;
     }
     if constexpr (R > 1) {
+        PSGD_STAMP(0);
         const int r = u.r;
         const int64_t k = u.k;
         const int tid = threadIdx.x;
@@ -306,12 +327,14 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                 }
             }
         }
+        PSGD_STAMP(1);
         int phase = 0;
         float tau[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             tau[j] = 0.f;
             if (j >= r) continue;
+            PSGD_STAMP(2 + 2 * j);
             float v2[2] = {0.f, 0.f};  // sum_{i>j} A[i][j]^2, alpha = A[j][j]
 #pragma unroll
             for (int q = 0; q < RPT; ++q) {
@@ -321,6 +344,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                 if (i == j) v2[1] = x;
             }
             wg_sum<2, kOrthWaves>(v2, red, phase);
+            PSGD_STAMP(3 + 2 * j);
             const float alpha = v2[1];
             float tj = 0.f;
             if (v2[0] != 0.f) {
@@ -356,6 +380,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                 }
             }
         }
+        PSGD_STAMP(40);
         // org2r: Q = H_0 ... H_{r-1} I[:, :r]
 #pragma unroll
         for (int j = R - 1; j >= 0; --j) {
@@ -389,6 +414,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                 else if (i < j) A[q][j] = 0.f;
             }
         }
+        PSGD_STAMP(41);
         float* __restrict__ hx = a.hx + u.off;
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
@@ -402,7 +428,378 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                     }
             }
         }
+        PSGD_STAMP(42);
     }
+}
+
+// ------------------------------------------------- WY-form Householder (fast path) ----
+// LAPACK geqr2 + org2r semantics with two latency cuts (stamps: each workgroup reduction
+// costs ~1k cycles, the arithmetic is negligible):
+//  * per column j ONE reduction gathers ||A[j+1:, j]||^2, alpha = A[j][j], the dots
+//    d_c = A[j+1:, j] . A[j+1:, c] and A[j][c] (c > j): w_c = A[j][c] + scal * d_c is the
+//    same quantity as LAPACK's slarf w = v^T C with v = [1; scal * A[j+1:, j]];
+//  * Q = H_0 ... H_{r-1} [I; 0] = [I; 0] - V T V1^T (compact WY, LAPACK slarft: T upper
+//    triangular from tau and V^T V), i.e. ONE more reduction instead of r - 1 in org2r.
+// NW = waves per panel: NW = 1 -> one wave per panel (4 panels per 256-thread workgroup,
+// no barriers); NW = 4/8/16 -> the whole workgroup of 64*NW threads works on one panel
+// (rows tid + 64*NW*q, cross-wave sums through LDS). More waves per panel means fewer rows
+// per wave and several waves per SIMD to hide each other's latency.
+template <int NV, int NW>
+__device__ __forceinline__ void grp_sum(float (&v)[NV], float* red, int& phase) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_allsum(v[i]);
+    if constexpr (NW > 1) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        float* buf = red + phase * (NW + 1) * NV;
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) buf[wave * NV + i] = v[i];
+        }
+        __syncthreads();
+        if constexpr (NW * NV <= 64) {  // few partials: every thread adds them itself
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                float sum = buf[i];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) sum += buf[w * NV + i];
+                v[i] = sum;
+            }
+        } else {  // thread i adds partial i over the waves (same order), then all read
+            if (threadIdx.x < NV) {
+                float sum = buf[threadIdx.x];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) sum += buf[w * NV + threadIdx.x];
+                buf[NW * NV + threadIdx.x] = sum;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < NV; ++i) v[i] = buf[NW * NV + i];
+        }
+        phase ^= 1;
+    }
+}
+
+// rank-1 unit handled by the NW waves of its panel group
+template <int NW>
+__device__ void joint_norm_grp(const OrthArgs& a, const OrthUnit& u, float* red) {
+    constexpr int NT = 64 * NW;
+    const int t = NW == 1 ? (threadIdx.x & 63) : threadIdx.x;
+    float* __restrict__ st = a.state + u.off;
+    float* __restrict__ hx = a.hx + u.off;
+    float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+    const int64_t total = u.k * u.count;
+    constexpr int U = 8;
+    float part[1] = {0.f};
+    for (int64_t base = t; base < total; base += int64_t(U) * NT) {
+        float x[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) x[q] = st[base + q * NT < total ? base + q * NT : 0];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            keep(x[q]);
+            part[0] = fmaf(base + q * NT < total ? x[q] : 0.f, base + q * NT < total ? x[q] : 0.f, part[0]);
+        }
+    }
+    int phase = 0;
+    grp_sum<1, NW>(part, red, phase);
+    const float nrm = sqrtf(part[0]);
+    const float d = nrm > 1e-16f ? nrm : 1e-16f;  // torch.maximum(norm, eps)
+    for (int64_t base = t; base < total; base += int64_t(U) * NT) {
+        float x[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) x[q] = st[base + q * NT < total ? base + q * NT : 0];
+#pragma unroll
+        for (int q = 0; q < U; ++q) keep(x[q]);
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t i = base + q * NT;
+            if (i < total) {
+                if (sv) sv[i] = x[q];
+                const float y = x[q] / d;
+                st[i] = y;
+                hx[i] = y;
+            }
+        }
+    }
+}
+
+// a panel row of r floats: one 16-byte (or 8-byte) access when r == R in {2, 4, 8}
+template <int R>
+__device__ __forceinline__ void ld_row(const float* __restrict__ p, int r, float (&v)[R]) {
+    ld_factor<R>(gconst<float>(p), r, v);
+}
+template <int R>
+__device__ __forceinline__ void st_row(float* __restrict__ p, int r, const float (&v)[R]) {
+    const gptr<float> g = gmut<float>(p);
+    if constexpr (R % 4 == 0) {
+        if (r == R) {
+#pragma unroll
+            for (int c = 0; c < R; c += 4) {
+                const v4f x = {v[c], v[c + 1], v[c + 2], v[c + 3]};
+                *(gptr<v4f>)(g + c) = x;
+            }
+            return;
+        }
+    } else if constexpr (R == 2) {
+        if (r == 2) {
+            const v2f x = {v[0], v[1]};
+            *(gptr<v2f>)g = x;
+            return;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+        if (c < r) g[c] = v[c];
+}
+
+template <int R, int RPT, int NW>
+__global__ __launch_bounds__(NW == 1 ? kBlock : 64 * NW) void k_orth_wy(OrthArgs a, int nunits) {
+    constexpr int kRed = (2 * R + 2) > (2 * R * R) ? (2 * R + 2) : (2 * R * R);  // largest sum
+    __shared__ __attribute__((aligned(16))) float red[2 * (NW + 1) * kRed];
+    constexpr int NT = 64 * NW;  // threads per panel
+    const int unit = NW == 1 ? blockIdx.x * kWaves + (threadIdx.x >> 6) : blockIdx.x;
+    if (unit >= nunits) return;  // NW == 1 only: whole waves leave, no barrier follows
+    const OrthUnit u = a.units[unit];
+    if (u.r == 1) {
+        joint_norm_grp<NW>(a, u, red);
+        return;
+    }
+    PSGD_STAMP(0);
+    const int r = u.r;
+    const int k = int(u.k);
+    const int t = NW == 1 ? (threadIdx.x & 63) : threadIdx.x;
+    const int nq = (k + NT - 1) / NT;  // row slots in use (uniform); slot q holds row t + q*NT
+    float* __restrict__ st = a.state + u.off;
+    float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+    // Rows >= k are zero, so they add nothing to any sum and stay zero under every update;
+    // rows in slots q >= 1 are >= NT > R, i.e. strictly below every diagonal element: only
+    // slot 0 needs the diagonal cases (i == j / i < j).
+    float A[RPT][R];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {  // whole rows, from clamped (always valid) row indices
+        const int i = t + q * NT;
+        ld_row<R>(st + int64_t(i < k ? i : 0) * r, r, A[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int i = t + q * NT;
+#pragma unroll
+        for (int c = 0; c < R; ++c) {
+            keep(A[q][c]);
+            A[q][c] = i < k ? A[q][c] : 0.f;
+        }
+    }
+    if (sv) {
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int i = t + q * NT;
+            if (q < nq && i < k) st_row<R>(sv + int64_t(i) * r, r, A[q]);
+        }
+    }
+    PSGD_STAMP(1);
+    int phase = 0;
+    float tau[R];
+    // ---- geqr2: A <- R (rows < r) and V (strictly below the diagonal, unit diagonal implied)
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        tau[j] = 0.f;
+        if (j >= r) continue;
+        // v[0] = sum_{i>j} A[i][j]^2, v[1] = alpha, v[2+c] = d_c (c > j), v[2+R+c] = A[j][c] (c > j)
+        float v[2 + 2 * R];
+#pragma unroll
+        for (int e = 0; e < 2 + 2 * R; ++e) v[e] = 0.f;
+        {
+            const float x = A[0][j];
+            const float xb = t > j ? x : 0.f;
+            v[0] = xb * xb;
+            v[1] = t == j ? x : 0.f;
+#pragma unroll
+            for (int c = j + 1; c < R; ++c) {
+                v[2 + c] = xb * A[0][c];
+                v[2 + R + c] = t == j ? A[0][c] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int q = 1; q < RPT; ++q) {
+            if (q < nq) {  // uniform: unused row slots do nothing
+                const float x = A[q][j];
+                v[0] = fmaf(x, x, v[0]);
+    #pragma unroll
+                for (int c = j + 1; c < R; ++c) v[2 + c] = fmaf(x, A[q][c], v[2 + c]);
+            }
+        }
+        grp_sum<2 + 2 * R, NW>(v, red, phase);
+        const float alpha = v[1];
+        if (v[0] != 0.f) {  // LAPACK slarfg: xnorm == 0 -> tau = 0, H_j = I
+            const float beta = -copysignf(hypotf(alpha, sqrtf(v[0])), alpha);
+            const float tj = (beta - alpha) / beta;
+            const float scal = 1.f / (alpha - beta);
+            tau[j] = tj;
+            float w[R];
+#pragma unroll
+            for (int c = j + 1; c < R; ++c) w[c] = v[2 + R + c] + scal * v[2 + c];
+            {
+                const bool below = t > j;
+                const float vi = below ? A[0][j] * scal : (t == j ? 1.f : 0.f);
+                A[0][j] = below ? vi : (t == j ? beta : A[0][j]);
+#pragma unroll
+                for (int c = j + 1; c < R; ++c) A[0][c] -= tj * vi * w[c];
+            }
+#pragma unroll
+            for (int q = 1; q < RPT; ++q) {
+                if (q < nq) {  // uniform: unused row slots do nothing
+                    const float vi = A[q][j] * scal;
+                    A[q][j] = vi;
+    #pragma unroll
+                    for (int c = j + 1; c < R; ++c) A[q][c] -= tj * vi * w[c];
+                }
+            }
+        }
+    }
+    PSGD_STAMP(40);
+    // ---- slarft: T from tau and S = V^T V; V1 = rows 0..r-1 of V, broadcast in the same sum
+    float sv2[2 * R * R];  // [0, R*R): S[a][b] (a < b); [R*R, 2R*R): V[row a][col b]
+#pragma unroll
+    for (int e = 0; e < 2 * R * R; ++e) sv2[e] = 0.f;
+    {
+        float vr[R];  // row t of V (slot 0 holds the diagonal cases)
+#pragma unroll
+        for (int c = 0; c < R; ++c) vr[c] = (c < r) ? (t == c ? 1.f : (t > c ? A[0][c] : 0.f)) : 0.f;
+#pragma unroll
+        for (int a2 = 0; a2 < R; ++a2)
+#pragma unroll
+            for (int b = a2 + 1; b < R; ++b) sv2[a2 * R + b] = vr[a2] * vr[b];
+#pragma unroll
+        for (int a2 = 0; a2 < R; ++a2)
+#pragma unroll
+            for (int b = 0; b < R; ++b) sv2[R * R + a2 * R + b] = t == a2 ? vr[b] : 0.f;
+    }
+#pragma unroll
+    for (int q = 1; q < RPT; ++q) {
+        if (q < nq) {  // uniform: unused row slots do nothing
+    #pragma unroll
+            for (int a2 = 0; a2 < R; ++a2)
+    #pragma unroll
+                for (int b = a2 + 1; b < R; ++b) sv2[a2 * R + b] = fmaf(A[q][a2], A[q][b], sv2[a2 * R + b]);
+        }
+    }
+    grp_sum<2 * R * R, NW>(sv2, red, phase);
+    float T[R][R];
+#pragma unroll
+    for (int a2 = 0; a2 < R; ++a2)
+#pragma unroll
+        for (int b = 0; b < R; ++b) T[a2][b] = 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if (j >= r) continue;
+        // T[0:j, j] = -tau_j * T[0:j, 0:j] * S[0:j, j];  T[j][j] = tau_j
+        float y[R];
+#pragma unroll
+        for (int a2 = 0; a2 < R; ++a2) y[a2] = a2 < j ? -tau[j] * sv2[a2 * R + j] : 0.f;
+#pragma unroll
+        for (int a2 = 0; a2 < R; ++a2) {
+            if (a2 >= j) continue;
+            float acc = 0.f;
+#pragma unroll
+            for (int b = 0; b < R; ++b)
+                if (b >= a2 && b < j) acc = fmaf(T[a2][b], y[b], acc);
+            T[a2][j] = acc;
+        }
+        T[j][j] = tau[j];
+    }
+    // M = T V1^T  (r x r):  M[l][c] = sum_b T[l][b] * V[c][b]
+    float M[R][R];
+#pragma unroll
+    for (int l = 0; l < R; ++l)
+#pragma unroll
+        for (int c = 0; c < R; ++c) {
+            float acc = 0.f;
+#pragma unroll
+            for (int b = 0; b < R; ++b) acc = fmaf(T[l][b], sv2[R * R + c * R + b], acc);
+            M[l][c] = acc;
+        }
+    // Q[i][c] = [i == c] - sum_l V[i][l] * M[l][c]
+    float* __restrict__ hx = a.hx + u.off;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        if (q < nq) {  // uniform: unused row slots do nothing
+            const int i = t + q * NT;
+            float vr[R];
+    #pragma unroll
+            for (int c = 0; c < R; ++c) {
+                if (q == 0)
+                    vr[c] = (c < r) ? (i == c ? 1.f : (i > c ? A[0][c] : 0.f)) : 0.f;
+                else
+                    vr[c] = A[q][c];  // c >= r columns are zero
+            }
+            float qrow[R];
+    #pragma unroll
+            for (int c = 0; c < R; ++c) {
+                float acc = 0.f;
+    #pragma unroll
+                for (int l = 0; l < R; ++l) acc = fmaf(vr[l], M[l][c], acc);
+                qrow[c] = (i == c ? 1.f : 0.f) - acc;
+            }
+            if (i < k) {
+                st_row<R>(st + int64_t(i) * r, r, qrow);
+                st_row<R>(hx + int64_t(i) * r, r, qrow);
+            }
+        }
+    }
+    PSGD_STAMP(42);
+}
+
+// register budget of the WY kernel (checked with -Rpass-analysis=kernel-resource-usage:
+// no spills for these pairs at the launch bounds used)
+__host__ __device__ constexpr bool orth_wy_ok(int R, int RPT) {
+    return R <= 4 ? R * RPT <= 32 : R * RPT <= 16;
+}
+
+template <int R, int RPT, int NW>
+void launch_orth_wy_one(const OrthArgs& a, int nunits, hipStream_t s) {
+    if constexpr (orth_wy_ok(R, RPT) && !(R == 8 && NW == 16)) {  // R=8 x 1024 threads spills
+        const int blocks = NW == 1 ? (nunits + kWaves - 1) / kWaves : nunits;
+        k_orth_wy<R, RPT, NW><<<blocks, NW == 1 ? kBlock : 64 * NW, 0, s>>>(a, nunits);
+    }
+}
+
+template <int R, int NW>
+hipError_t launch_orth_wy_r(int rpt, const OrthArgs& a, int nunits, hipStream_t s) {
+    switch (rpt) {
+        case 1: launch_orth_wy_one<R, 1, NW>(a, nunits, s); break;
+        case 2: launch_orth_wy_one<R, 2, NW>(a, nunits, s); break;
+        case 4: launch_orth_wy_one<R, 4, NW>(a, nunits, s); break;
+        case 8: launch_orth_wy_one<R, 8, NW>(a, nunits, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_orth_wy_nw(int nw, int rpt, const OrthArgs& a, int nunits, hipStream_t s) {
+    switch (nw) {
+        case 1: return launch_orth_wy_r<R, 1>(rpt, a, nunits, s);
+        case 4: return launch_orth_wy_r<R, 4>(rpt, a, nunits, s);
+        case 8: return launch_orth_wy_r<R, 8>(rpt, a, nunits, s);
+        default: return launch_orth_wy_r<R, 16>(rpt, a, nunits, s);
+    }
+}
+
+// Picks the fast WY kernel when the panel slice fits in registers; returns false otherwise.
+// Waves per panel: as few as keep every wave at <= 8 rows (1 wave up to 512 rows ... 16 waves
+// up to 8192 rows).
+bool launch_orth_wy(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s, hipError_t* err) {
+    if (R < 2 || R > 8) return false;
+    const int nw_max = R == 8 ? 8 : 16;  // R = 8 needs > 128 VGPRs: no 1024-thread groups
+    int nw = 1;
+    while (nw < nw_max && int64_t(64) * nw * 8 < kmax) nw = nw == 1 ? 4 : nw * 2;
+    int64_t rpt = 1;
+    while (rpt * 64 * nw < kmax) rpt <<= 1;
+    if (rpt > 8 || !orth_wy_ok(R, int(rpt))) return false;
+    *err = R == 2 ? launch_orth_wy_nw<2>(nw, int(rpt), a, nunits, s)
+         : R == 4 ? launch_orth_wy_nw<4>(nw, int(rpt), a, nunits, s)
+                  : launch_orth_wy_nw<8>(nw, int(rpt), a, nunits, s);
+    return true;
 }
 
 // Register budget: 1024-thread workgroups get at most 128 VGPRs, so the panel slice a
@@ -445,11 +842,21 @@ hipError_t launch_orth_r(int R, const OrthArgs& a, int nunits, int64_t lds_float
     return hipGetLastError();
 }
 
+static bool env_orth_wy() {
+    static const bool on = [] {
+        const char* v = std::getenv("PSGD_ORTH_WY");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
     // register-resident path when the longest rank>1 panel fits RPT * R <= 128 floats/thread
     int64_t rpt = 1;
     while (rpt * kOrthThreads < kmax) rpt <<= 1;
     if (R == 1) return launch_orth_reg_r<1>(1, a, nunits, s);
+    hipError_t err = hipSuccess;
+    if (env_orth_wy() && launch_orth_wy(a, nunits, R, kmax, s, &err)) return err;
     if (rpt <= 16 && orth_reg_ok(R, int(rpt))) {
         switch (R) {
             case 2: return launch_orth_reg_r<2>(int(rpt), a, nunits, s);
