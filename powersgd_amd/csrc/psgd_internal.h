@@ -86,6 +86,20 @@ struct ReduceArgs {
     float* yloc;         // history copy of the local factor
     float* state;        // reference-visible state buffer (the out-factor)
     int32_t even;
+    int32_t nmain;       // items[0, nmain) reduce the out-factor
+    // Rank-1 fused normalisation (world size 1, iteration >= 1): the product ran on the RAW
+    // in-factor `raw` (the previous iteration's reduced out-factor); its group norm comes
+    // from the previous reduction's sum-of-squares partials `ss_in` (per item, group g's
+    // items are grng_in[g] = [begin, end)). The reduction divides by it, and the extra
+    // items nitems[0, nnorm) write the normalised in-factor to `xstate` and `hx`.
+    const float* ss_in;
+    const int32_t* grng_in;
+    const RedItem* nitems;
+    int32_t nnorm;
+    const float* raw;
+    float* xstate;
+    float* hx;
+    float* ss_out;       // per-item sum of squares of this reduction's output (or null)
 };
 
 struct OrthArgs {

@@ -160,12 +160,14 @@ struct psgd_plan {
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
     int64_t tiles_cap = 0, tiles_om_cap = 0;
     std::vector<RedItem> red_even, red_odd;
+    std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
     std::vector<OrthUnit> units_p, units_q;
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_floats = 0;
     double unc_floats = 0, comp_floats = 0;
     size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_red_even = 0,
-           o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, ws_bytes = 0;
+           o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, o_grng_even = 0,
+           o_grng_odd = 0, o_ss = 0, ss_stride = 0, ws_bytes = 0;
     bool bound = false;
     int device = -1;
     float* P = nullptr;
@@ -442,8 +444,16 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
+        if (i == 0 || p->mats[i - 1].group != md.group) {
+            p->grng_even.push_back(int32_t(p->red_even.size()));
+            p->grng_even.push_back(0);
+            p->grng_odd.push_back(int32_t(p->red_odd.size()));
+            p->grng_odd.push_back(0);
+        }
         for (int64_t s = 0; s < md.m * md.r; s += kBlock) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
         for (int64_t s = 0; s < md.n * md.r; s += kBlock) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
+        p->grng_even.back() = int32_t(p->red_even.size());
+        p->grng_odd.back() = int32_t(p->red_odd.size());
     }
     p->set_vec(p->base_vec);
 
@@ -462,6 +472,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
     p->o_units_q = carve(p->units_q.size() * sizeof(OrthUnit));
+    p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
+    p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
+    p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
+    p->o_ss = carve(2 * p->ss_stride * sizeof(float));
     p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * sizeof(float));
     p->o_part = carve(size_t(p->part_floats) * sizeof(float));
     p->ws_bytes = off;
@@ -537,6 +551,8 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
+    if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
+    if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
     p->bound = true;
     return PSGD_OK;
 }
@@ -548,30 +564,38 @@ int psgd_out_factor(const psgd_plan* p, int64_t step, int32_t it, int32_t* which
     return PSGD_OK;
 }
 
-int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, void* stream) {
-    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
-    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
-    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
-    DevScope scope(p->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
+// World size 1 inside psgd_aggregate, every group rank 1, iteration >= 1: the joint-norm
+// orthonormalisation of the in-factor is folded into the neighbouring reductions (no
+// orthonormalisation launch): the previous reduction leaves per-item sums of squares, the
+// product runs on the raw in-factor, and this iteration's reduction divides by the norm and
+// writes the normalised in-factor (reference powersgd.py:186-188 + orthogonalization.py:5-6).
+static bool fused_norm(const psgd_plan* p, bool fuse, int it) {
+    return fuse && p->rbucket == 1 && it >= 1;
+}
+
+static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
+                         bool fuse) {
     if (int st = refresh_pointers(p, grads, s)) return st;
     const bool even = p->even(step, it);
     float* in = even ? p->P : p->Q;
     float* out = even ? p->Q : p->P;
+    const bool fused = fused_norm(p, fuse, it);
 
-    OrthArgs oa{};
-    oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
-    oa.state = in;
-    oa.hx = p->hist(0, it);
-    oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
-    const int nunits = int(even ? p->units_p.size() : p->units_q.size());
-    PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+    if (!fused) {
+        OrthArgs oa{};
+        oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
+        oa.state = in;
+        oa.hx = p->hist(0, it);
+        oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
+        const int nunits = int(even ? p->units_p.size() : p->units_q.size());
+        PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+    }
 
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
     pa.tiles = p->dev<Tile>(p->o_tiles);
     pa.grads = p->dev<void* const>(p->o_ptrs);
-    pa.x = p->hist(0, it);
+    pa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);  // fused: the raw reduced factor
     pa.part = p->dev<float>(p->o_part);
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
@@ -595,19 +619,32 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
     ra.yloc = p->hist(1, it);
     ra.state = out;
     ra.even = even ? 1 : 0;
-    const int nitems = int(even ? p->red_even.size() : p->red_odd.size());
-    PSGD_HIP(launch_reduce(ra, nitems, s));
+    ra.nmain = int(even ? p->red_even.size() : p->red_odd.size());
+    float* ss = p->dev<float>(p->o_ss);
+    if (fused) {  // in-factor items: the other parity's item list (in-factor side)
+        ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
+        ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
+        ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even);
+        ra.nnorm = int(even ? p->red_odd.size() : p->red_even.size());
+        ra.raw = p->hist(1, it - 1);
+        ra.xstate = in;
+        ra.hx = p->hist(0, it);
+    }
+    if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters) ra.ss_out = ss + size_t(it & 1) * p->ss_stride;
+    PSGD_HIP(launch_reduce(ra, ra.nmain + ra.nnorm, s));
     return PSGD_OK;
 }
 
-int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
-                    void* stream) {
-    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, void* stream) {
+    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
-    if (step < 0 || world < 1) return fail(PSGD_ERR_VALUE, "step/world size out of range");
-    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
     DevScope scope(p->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    return compress_impl(p, grads, step, it, static_cast<hipStream_t>(stream), false);
+}
+
+static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
+                           hipStream_t s, bool fuse) {
     if (int st = refresh_pointers(p, grads, s)) return st;
     const int I = p->iters;
     ApplyArgs aa{};
@@ -620,7 +657,8 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     for (int k = 0; k < kMaxTerms; ++k) aa.apx.p[k] = aa.apx.q[k] = nullptr;
     for (int k = 0; k < I; ++k) {
         const bool e = p->even(step, k);
-        float* ybar = k + 1 < I ? p->hist(2, k) : last;
+        // fused (world 1): the reduced factor was never copied to hist(2): use hist(1)
+        float* ybar = k + 1 < I ? p->hist(fused_norm(p, fuse, k + 1) ? 1 : 2, k) : last;
         aa.apx.p[k] = e ? p->hist(0, k) : ybar;
         aa.apx.q[k] = e ? ybar : p->hist(0, k);
     }
@@ -640,6 +678,16 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
     if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
     return PSGD_OK;
+}
+
+int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
+                    void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0 || world < 1) return fail(PSGD_ERR_VALUE, "step/world size out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    DevScope scope(p->device);
+    return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false);
 }
 
 int psgd_plan_set_timing(psgd_plan* p, int32_t enable) {
@@ -666,10 +714,16 @@ int psgd_plan_timing_read(psgd_plan* p, double* total_ms, int32_t* launches) {
 }
 
 int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, void* stream) {
-    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;
     for (int it = 0; it < p->iters; ++it)
-        if (int st = psgd_compress(p, grads, step, it, stream)) return st;
-    return psgd_decompress(p, grads, out, step, 1, stream);
+        if (int st = compress_impl(p, grads, step, it, s, fuse)) return st;
+    return decompress_impl(p, grads, out, step, 1, s, fuse);
 }
 
 // ------------------------------------------------------------------ flat pack ------

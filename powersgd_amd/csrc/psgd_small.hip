@@ -874,32 +874,71 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipSt
 // ---------------------------------------------------------------- partial reduction
 // Sums the partials of each factor element in a FIXED order (row chunks for even
 // iterations, column strips for odd ones): bitwise reproducible, no atomics.
+
+// Joint norm of a rank-1 group from per-item sums of squares (reference
+// orthogonalization.py:5-6: max(||x||, eps)); every workgroup evaluates the same fixed
+// order (lane-strided partial sums, then the DPP/permlane wave tree), so all agree bitwise.
+__device__ __forceinline__ float fused_group_norm(const ReduceArgs& a, int group) {
+    const int lane = threadIdx.x & 63;
+    const int b = a.grng_in[2 * group], e = a.grng_in[2 * group + 1];
+    float ss = 0.f;
+    for (int i = b + lane; i < e; i += 64) ss += a.ss_in[i];
+    const float nrm = sqrtf(wave_allsum(ss));
+    return nrm > 1e-16f ? nrm : 1e-16f;
+}
+
 __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
+    __shared__ float red[kWaves];
+    if (int(blockIdx.x) >= a.nmain) {  // fused normalisation of the in-factor (rank 1)
+        const RedItem it = a.nitems[blockIdx.x - a.nmain];
+        const MatDesc d = a.mats[it.mat];
+        const float dn = fused_group_norm(a, d.group);
+        const int64_t len = a.even ? d.n : d.m;
+        const int64_t e = int64_t(it.start) + threadIdx.x;
+        if (e < len) {
+            const int64_t i = (a.even ? d.poff : d.qoff) + e;
+            const float x = a.raw[i] / dn;  // matrix.div_(max(norm, eps))
+            a.xstate[i] = x;
+            a.hx[i] = x;
+        }
+        return;
+    }
     const RedItem it = a.items[blockIdx.x];
     const MatDesc d = a.mats[it.mat];
+    const float dn = a.ss_in ? fused_group_norm(a, d.group) : 1.f;
     const int64_t len = (a.even ? d.m : d.n) * d.r;
     const int64_t e = int64_t(it.start) + threadIdx.x;
-    if (e >= len) return;
-    const float* p = a.part + (a.even ? d.part_even : d.part_odd) + e;
-    const int np = a.even ? d.nchunk : d.odd_nstrip;
-    const int64_t dst = (a.even ? d.qoff : d.poff) + e;
-    // fixed summation order c = 0, 1, ..., np-1; loads issued 8 at a time
-    float s = p[0];
-    int c = 1;
-    for (; c + 8 <= np; c += 8) {
-        float v[8];
+    float s = 0.f;
+    if (e < len) {
+        const float* p = a.part + (a.even ? d.part_even : d.part_odd) + e;
+        const int np = a.even ? d.nchunk : d.odd_nstrip;
+        const int64_t dst = (a.even ? d.qoff : d.poff) + e;
+        // fixed summation order c = 0, 1, ..., np-1; loads issued 8 at a time
+        s = p[0];
+        int c = 1;
+        for (; c + 8 <= np; c += 8) {
+            float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q) * len];
+            for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q) * len];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s += v[q];
+            for (int q = 0; q < 8; ++q) s += v[q];
+        }
+        for (; c < np; ++c) s += p[int64_t(c) * len];
+        if (a.ss_in) s = s / dn;  // G^T (x / d) == (G^T x) / d up to rounding
+        a.yloc[dst] = s;
+        a.state[dst] = s;
     }
-    for (; c < np; ++c) s += p[int64_t(c) * len];
-    a.yloc[dst] = s;
-    a.state[dst] = s;
+    if (a.ss_out) {  // this output is the next iteration's in-factor: its sum of squares
+        float v = wave_allsum(s * s);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) red[wave] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) a.ss_out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
 }
 
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
-    k_reduce<<<nitems, kBlock, 0, s>>>(a);
+    k_reduce<<<nitems, kBlock, 0, s>>>(a);  // nitems = nmain + nnorm
     return hipGetLastError();
 }
 
