@@ -39,6 +39,8 @@ struct Tile {
 };
 
 // Reduction item for the partial-sum pass: 256 consecutive factor elements of one matrix.
+constexpr int kRedElems = 64;  // factor elements per reduction item (one per lane)
+
 struct RedItem {
     int32_t mat, start;
 };

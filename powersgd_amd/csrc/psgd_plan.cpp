@@ -450,8 +450,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
             p->grng_odd.push_back(int32_t(p->red_odd.size()));
             p->grng_odd.push_back(0);
         }
-        for (int64_t s = 0; s < md.m * md.r; s += kBlock) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
-        for (int64_t s = 0; s < md.n * md.r; s += kBlock) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
+        for (int64_t s = 0; s < md.m * md.r; s += kRedElems) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
+        for (int64_t s = 0; s < md.n * md.r; s += kRedElems) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
         p->grng_even.back() = int32_t(p->red_even.size());
         p->grng_odd.back() = int32_t(p->red_odd.size());
     }

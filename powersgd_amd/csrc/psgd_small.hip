@@ -887,14 +887,19 @@ __device__ __forceinline__ float fused_group_norm(const ReduceArgs& a, int group
     return nrm > 1e-16f ? nrm : 1e-16f;
 }
 
+// One item = kRedElems (64) consecutive elements of one factor; wave w adds the partials
+// [w*np/4, (w+1)*np/4) of each element in order, then wave 0 adds the four wave sums in
+// order: every element is summed in the same fixed order on every run.
 __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
-    __shared__ float red[kWaves];
+    __shared__ float red[kWaves * kRedElems];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (int(blockIdx.x) >= a.nmain) {  // fused normalisation of the in-factor (rank 1)
+        if (wave != 0) return;
         const RedItem it = a.nitems[blockIdx.x - a.nmain];
         const MatDesc d = a.mats[it.mat];
         const float dn = fused_group_norm(a, d.group);
-        const int64_t len = a.even ? d.n : d.m;
-        const int64_t e = int64_t(it.start) + threadIdx.x;
+        const int64_t len = (a.even ? d.n : d.m) * d.r;
+        const int64_t e = int64_t(it.start) + lane;
         if (e < len) {
             const int64_t i = (a.even ? d.poff : d.qoff) + e;
             const float x = a.raw[i] / dn;  // matrix.div_(max(norm, eps))
@@ -905,35 +910,36 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     }
     const RedItem it = a.items[blockIdx.x];
     const MatDesc d = a.mats[it.mat];
-    const float dn = a.ss_in ? fused_group_norm(a, d.group) : 1.f;
     const int64_t len = (a.even ? d.m : d.n) * d.r;
-    const int64_t e = int64_t(it.start) + threadIdx.x;
+    const int64_t e = int64_t(it.start) + lane;
+    const int64_t ec = e < len ? e : 0;
+    const int np = a.even ? d.nchunk : d.odd_nstrip;
+    const int c0 = wave * np / kWaves, c1 = (wave + 1) * np / kWaves;
+    const float* p = a.part + (a.even ? d.part_even : d.part_odd) + ec;
     float s = 0.f;
-    if (e < len) {
-        const float* p = a.part + (a.even ? d.part_even : d.part_odd) + e;
-        const int np = a.even ? d.nchunk : d.odd_nstrip;
-        const int64_t dst = (a.even ? d.qoff : d.poff) + e;
-        // fixed summation order c = 0, 1, ..., np-1; loads issued 8 at a time
-        s = p[0];
-        int c = 1;
-        for (; c + 8 <= np; c += 8) {
-            float v[8];
+    for (int c = c0; c < c1; c += 8) {  // loads issued 8 at a time (clamped, unconditional)
+        float v[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q) * len];
+        for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) s += v[q];
+        for (int q = 0; q < 8; ++q) {
+            keep(v[q]);
+            s += c + q < c1 ? v[q] : 0.f;
         }
-        for (; c < np; ++c) s += p[int64_t(c) * len];
-        if (a.ss_in) s = s / dn;  // G^T (x / d) == (G^T x) / d up to rounding
+    }
+    red[wave * kRedElems + lane] = s;
+    __syncthreads();
+    if (wave != 0) return;
+    s = ((red[lane] + red[kRedElems + lane]) + red[2 * kRedElems + lane]) + red[3 * kRedElems + lane];
+    if (a.ss_in) s = s / fused_group_norm(a, d.group);  // G^T (x / d) == (G^T x) / d up to rounding
+    if (e < len) {
+        const int64_t dst = (a.even ? d.qoff : d.poff) + e;
         a.yloc[dst] = s;
         a.state[dst] = s;
     }
     if (a.ss_out) {  // this output is the next iteration's in-factor: its sum of squares
-        float v = wave_allsum(s * s);
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane == 0) red[wave] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) a.ss_out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+        const float v = wave_allsum(e < len ? s * s : 0.f);
+        if (lane == 0) a.ss_out[blockIdx.x] = v;
     }
 }
 
