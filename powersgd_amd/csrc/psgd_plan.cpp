@@ -116,6 +116,8 @@ OddGeom odd_geometry(int64_t n, int64_t m, int64_t tile_elems) {
     g.sw = int(std::min<int64_t>(256, round_up(m, 16)));
     const int64_t rows_pass = 16 * kWaves;
     int64_t groups = std::max<int64_t>(1, tile_elems / (rows_pass * g.sw));
+    // a small matrix must still spread over several workgroups (as geometry())
+    groups = std::min(groups, std::max<int64_t>(1, ((n + 7) / 8 + rows_pass - 1) / rows_pass));
     int64_t cr = std::min(groups * rows_pass, round_up(n, rows_pass));
     g.chunk_rows = int(cr);
     g.nstrip = int((m + g.sw - 1) / g.sw);
@@ -199,6 +201,7 @@ struct psgd_plan {
         tiles_ov.clear();
         tiles_om.clear();
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
+        const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
         for (size_t i = 0; i < mats.size(); ++i) {
             MatDesc& d = mats[i];
             const Geom g = geometry(d.n, d.m, d.r, vec[i], tile_elems);
@@ -207,14 +210,20 @@ struct psgd_plan {
             d.nstrip = g.nstrip;
             d.nchunk = g.nchunk;
             d.chunk_rows = g.chunk_rows;
-            d.odd_mfma = (use_mfma && d.r <= 16) ? 1 : 0;
+            const OddGeom og = odd_geometry(d.n, d.m, tile_elems);
+            // the MFMA kernel addresses a tile through a buffer descriptor (< 2^31 bytes)
+            const int64_t span = ((int64_t(og.chunk_rows) - 1) * d.m + og.sw) * (dtype == PSGD_BF16 ? 2 : 4);
+            // r <= 4: every odd tile stays in ONE k_product<odd> launch (row layout with a
+            // reduce-scatter on full-width strips, lane sums on narrow ones); the MFMA kernel
+            // pays for itself only for wider factors (16 output columns per instruction)
+            const bool valu = use_rows && d.r <= 4;
+            d.odd_mfma = (use_mfma && !valu && d.r <= 16 && span < (int64_t(1) << 31)) ? 1 : 0;
             for (int c = 0; c < g.nchunk; ++c)
                 for (int s = 0; s < g.nstrip; ++s) {
                     tiles.push_back(Tile{int32_t(i), s, c, 0});
                     if (!d.odd_mfma) tiles_ov.push_back(Tile{int32_t(i), s, c, 0});
                 }
             if (d.odd_mfma) {
-                const OddGeom og = odd_geometry(d.n, d.m, tile_elems);
                 d.odd_sw = og.sw;
                 d.odd_chunk_rows = og.chunk_rows;
                 d.odd_nstrip = og.nstrip;

@@ -157,13 +157,16 @@ __device__ __forceinline__ float swap32_sum(float v) {
     const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
-// sum over the lanes that share lane / L (partners lane ^ s, s < L); L = 1..64, power of 2
+// sum over the lanes that share lane / L (aligned groups of L lanes); L = 1..64, power of
+// 2. Groups smaller than a 16-lane row need partners INSIDE the group: quad_perm xor 1 /
+// xor 2, then row_half_mirror (l -> 7 - l) and row_mirror (l -> 15 - l), whose partner lies
+// in the other half of the 8 / 16 group (all of whose lanes already hold the same sum).
 __device__ __forceinline__ float sum_within(float v, int L) {
     float t;
-    t = v + dpp<0x121>(v); v = L > 1 ? t : v;
-    t = v + dpp<0x122>(v); v = L > 2 ? t : v;
-    t = v + dpp<0x124>(v); v = L > 4 ? t : v;
-    t = v + dpp<0x128>(v); v = L > 8 ? t : v;
+    t = v + dpp<0xB1>(v);  v = L > 1 ? t : v;   // quad_perm [1,0,3,2]
+    t = v + dpp<0x4E>(v);  v = L > 2 ? t : v;   // quad_perm [2,3,0,1]
+    t = v + dpp<0x141>(v); v = L > 4 ? t : v;   // row_half_mirror
+    t = v + dpp<0x140>(v); v = L > 8 ? t : v;   // row_mirror
     t = swap16_sum(v);     v = L > 16 ? t : v;
     t = swap32_sum(v);     v = L > 32 ? t : v;
     return v;
@@ -210,6 +213,180 @@ __device__ __forceinline__ TileGeom tile_geom(const MatDesc& d, const Tile& t) {
 }
 
 constexpr int kUnroll = 4;  // rows in flight per lane
+
+// ------------------------------------------------- odd product, row layout (VALU) --
+// For full-width strips (256 columns = 64 lanes x 4) and r <= 4: a wave takes 16 rows; each
+// wave-instruction reads 1 KB of ONE row; lane l forms the r partial dots of its 4 columns
+// for each row (16 r values), and a butterfly REDUCE-SCATTER over the 64 lanes leaves every
+// lane with the total of one (row, column) item. Halving step on lane bit b: the value list
+// is split in halves (a = first, b = second); lanes with bit b = 0 keep a, the others keep
+// b, and each receives its partner's copy of the half it keeps. Bits 5 and 4 use the gfx950
+// half-row swaps (v_permlane32_swap / v_permlane16_swap: one instruction per pair), bit 3
+// DPP row_ror:8 (= xor 8), bit 2 row_ror:12 / row_ror:4 (the partner above / below), bits 1
+// and 0 DPP quad_perm xor patterns. ~40 VALU per 16 rows at r = 1, against 16 dependent
+// 16x16x4 MFMAs of which 15/16 of the columns are padding.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+constexpr int kDppXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;  // quad_perm [2,3,0,1]
+
+template <int NV>
+__device__ __forceinline__ void halve_swap32(float (&v)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV / 2; ++i) {
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + NV / 2]), false, false);
+        v[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+}
+template <int NV>
+__device__ __forceinline__ void halve_swap16(float (&v)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV / 2; ++i) {
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + NV / 2]), false, false);
+        v[i] = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+    }
+}
+// lane bit B in {0, 1, 2, 3}: DPP partner exchange inside 16-lane rows
+template <int NV, int B>
+__device__ __forceinline__ void halve_dpp(float (&v)[NV], int lane) {
+    const bool hi = (lane >> B) & 1;
+#pragma unroll
+    for (int i = 0; i < NV / 2; ++i) {
+        const float a = v[i], b = v[i + NV / 2];
+        const float kept = hi ? b : a, send = hi ? a : b;
+        float recv;
+        if constexpr (B == 3) recv = dppf<0x128>(send);                      // row_ror:8
+        else if constexpr (B == 2) {
+            // row_ror:N delivers lane (l - N) mod 16: low lanes take l + 4 (ror 12), high
+            // ones l - 4 (ror 4). Both moves must run with every lane active (a DPP read
+            // from a disabled lane yields 0): pinned before the select, so the compiler
+            // cannot turn the select into a divergent branch around them.
+            float r4 = dppf<0x124>(send), r12 = dppf<0x12C>(send);
+            keep(r4);
+            keep(r12);
+            recv = hi ? r4 : r12;
+        }
+        else if constexpr (B == 1) recv = dppf<kDppXor2>(send);
+        else recv = dppf<kDppXor1>(send);
+        v[i] = kept + recv;
+    }
+}
+
+// NV = 16 R values per lane -> one total per lane (lanes sharing lane >> (6 - log2 NV) agree)
+template <int NV>
+__device__ __forceinline__ float reduce_scatter(float (&v)[NV], int lane) {
+    halve_swap32<NV>(v);
+    halve_swap16<NV / 2>(reinterpret_cast<float(&)[NV / 2]>(v));
+    halve_dpp<NV / 4, 3>(reinterpret_cast<float(&)[NV / 4]>(v), lane);
+    halve_dpp<NV / 8, 2>(reinterpret_cast<float(&)[NV / 8]>(v), lane);
+    if constexpr (NV >= 32) halve_dpp<NV / 16, 1>(reinterpret_cast<float(&)[NV / 16]>(v), lane);
+    if constexpr (NV >= 64) halve_dpp<NV / 32, 0>(reinterpret_cast<float(&)[NV / 32]>(v), lane);
+    float t = v[0];
+    if constexpr (NV < 32) t = t + dppf<kDppXor2>(t);  // remaining lanes hold partial sums
+    if constexpr (NV < 64) t = t + dppf<kDppXor1>(t);
+    return t;
+}
+
+template <typename T, int R, int K>
+__device__ __forceinline__ void odd_rows_tile(const ProductArgs& a, const MatDesc& d, const Tile& t) {
+    static_assert(R <= 4, "row-layout odd product: r <= 4");
+    constexpr int RB = R == 4 ? 8 : 16;                 // rows per batch
+    constexpr int NV = RB * R;                          // values reduced per batch (16 or 32)
+    constexpr int SH = NV == 16 ? 2 : 1;                // lanes >> SH share one item
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = d.r;
+    const int64_t n = d.n, m = d.m;
+    const int32_t col0 = t.strip * 256 + 4 * lane;
+    const bool active = col0 < m;
+    const int32_t ccol = active ? col0 : 0;
+    const int64_t row_begin = int64_t(t.chunk) * d.chunk_rows;
+    const int64_t row_end = n < row_begin + d.chunk_rows ? n : row_begin + d.chunk_rows;
+    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
+    const int nres = K >= 0 ? K : a.nres;
+    constexpr int KC = K > 0 ? K : 1;
+
+    float xq[4][R];  // X[col][c] of this lane's columns (zero when inactive)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ld_factor<R>(gconst<float>(a.x) + d.qoff + (ccol + v) * r, r, xq[v]);
+    float bq[KC][4][R];
+    if constexpr (K > 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (ccol + v) * r, r, bq[k][v]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int c = 0; c < R; ++c) xq[v][c] = active ? xq[v][c] : 0.f;
+
+    for (int64_t i0 = row_begin + wave * RB; i0 < row_end; i0 += kWaves * RB) {
+        const int nrow = row_end - i0 < RB ? int(row_end - i0) : RB;
+        // error-feedback rows P_k[i0 .. i0 + RB) (RB * r <= 32 floats, contiguous): lane l
+        // holds element l; row u's values are broadcast with readlane (wave-uniform)
+        float pk[KC];
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int e = lane < nrow * r ? lane : 0;
+                pk[k] = gconst<float>(a.res.p[k])[d.poff + i0 * r + e];
+            }
+        }
+        float x[RB][4];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int64_t i = i0 + u;
+            Io<T>::ld(G + (i < row_end ? i : row_begin) * m + ccol, x[u]);  // clamped, unconditional
+        }
+        float sv[NV];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) keep(x[u][v]);
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    float ap[R];
+#pragma unroll
+                    for (int c = 0; c < R; ++c) {
+                        const int src = u * r + (c < r ? c : 0);
+                        const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pk[k]), src < 64 ? src : 0));
+                        ap[c] = c < r ? w : 0.f;
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) x[u][v] = x[u][v] - dotr<R>(ap, bq[k][v]);
+                }
+            } else {
+                const int64_t ic = i0 + u < row_end ? i0 + u : row_begin;
+                for (int k = 0; k < nres; ++k) {  // many terms: factor rows from L1/L2
+                    float ap[R];
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic * r, r, ap);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        float b[R];
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (ccol + v) * r, r, b);
+                        x[u][v] = x[u][v] - dotr<R>(ap, b);
+                    }
+                }
+            }
+            const bool valid = u < nrow;
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                float s = x[u][0] * xq[0][c];
+#pragma unroll
+                for (int v = 1; v < 4; ++v) s = fmaf(x[u][v], xq[v][c], s);
+                sv[c * RB + u] = valid ? s : 0.f;
+            }
+        }
+        const float tot = reduce_scatter<NV>(sv, lane);
+        const int item = lane >> SH, c = item / RB, u = item % RB;
+        if ((lane & ((1 << SH) - 1)) == 0 && c < r && u < nrow)
+            gmut<float>(a.part)[d.part_odd + (int64_t(t.strip) * n + i0 + u) * r + c] = tot;
+    }
+}
 
 // ------------------------------------------------------------------ product -------
 template <typename T, int R, int K, bool EVEN, int V>
@@ -331,6 +508,12 @@ __global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
     __shared__ float lds[EVEN ? kWaves * 64 * (R <= 8 ? 4 : 1) * R : 1];
     const Tile t = a.tiles[blockIdx.x];
     const MatDesc d = a.mats[t.mat];
+    if constexpr (!EVEN && R <= 4) {
+        if (d.vec && d.lanes == 64) {  // full-width strips: row layout + reduce-scatter
+            odd_rows_tile<T, R, K>(a, d, t);
+            return;
+        }
+    }
     if constexpr (R <= 8) {
         if (d.vec) {
             product_tile<T, R, K, EVEN, 4>(a, d, t, lds);
@@ -354,9 +537,57 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int kOddSW = 256;            // max MFMA strip width (columns)
 constexpr int kOddXT = kOddSW + 4;      // padded row of the transposed X strip in LDS
 
-template <typename T, int VEC, int RC, int K>
+// Gradient reads of the odd product go through a buffer descriptor that spans exactly the
+// tile's region (from the strip's first column of row0 to the strip's last column of the
+// tile's last row): the hardware range check returns 0 for rows past the tile, and a slot
+// whose columns lie past the strip gets offset kOob (also 0, and no memory traffic). Every
+// load is therefore unconditional, unclamped and unmasked.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOob = 0x80000000u;  // beyond every descriptor (num_records < 2^31)
+
+template <typename T>
+struct BufIo;
+
+template <>
+struct BufIo<float> {
+    static __device__ __forceinline__ void ld4(rsrc_t r, uint32_t off, float (&v)[4]) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        v[0] = __uint_as_float(x[0]); v[1] = __uint_as_float(x[1]);
+        v[2] = __uint_as_float(x[2]); v[3] = __uint_as_float(x[3]);
+    }
+    static __device__ __forceinline__ float ld1(rsrc_t r, uint32_t off) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    }
+};
+
+template <>
+struct BufIo<bf16_t> {
+    static __device__ __forceinline__ void ld4(rsrc_t r, uint32_t off, float (&v)[4]) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+        v[0] = __uint_as_float(x[0] << 16);
+        v[1] = __uint_as_float(x[0] & 0xffff0000u);
+        v[2] = __uint_as_float(x[1] << 16);
+        v[3] = __uint_as_float(x[1] & 0xffff0000u);
+    }
+    static __device__ __forceinline__ float ld1(rsrc_t r, uint32_t off) {
+        return __uint_as_float(uint32_t(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0)) << 16);
+    }
+};
+
+// A wave owns row blocks rb (16 rows each: rows row0 + 16 (wave + 4 rb) + ri) of the tile
+// and works in ROUNDS of 16 slots (one 16-byte load per lane each), all issued together:
+//   WIDE   (strip > 64 columns): a round = 1 row block x 16 k-steps (the whole strip row);
+//   NARROW (strip <= 64 columns): a round = 4 row blocks x 4 k-steps.
+// tile_elems <= 16384 makes a wave's whole share one round; the first round is issued
+// before the factor strips are staged in LDS.
+constexpr int kOddSlots = 16;
+
+template <typename T, int VEC, int RC, int K, bool WIDE>
 __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDesc& d, const Tile& t,
                                               float* xt, float* bs) {
+    constexpr int QN = WIDE ? 1 : 4;     // row blocks per round
+    constexpr int KN = kOddSlots / QN;   // k-steps per round
+    constexpr int s = sizeof(T);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int ri = lane & 15, cq = lane >> 4;
     const int r = d.r;
@@ -367,13 +598,134 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
     const int32_t sw = j_end - j_begin;
     const int64_t row0 = int64_t(t.chunk) * d.odd_chunk_rows;
     const int64_t row_end = n < row0 + d.odd_chunk_rows ? n : row0 + d.odd_chunk_rows;
-    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
     const int nt = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;
     constexpr int RP = 4 * RC;           // factor columns held per strip row in LDS
-    constexpr int U = 4;                 // k-steps (16 columns each) in flight per lane
     const bool cvalid = ri < r;
     const int cx = cvalid ? ri : 0;
+    const int nks = (sw + 15) >> 4;      // 16-column k-steps of the strip
+    const int nrb = int((row_end - row0 - wave * 16 + kWaves * 16 - 1) / (kWaves * 16));  // >= 0
+
+    const uint32_t nrec = uint32_t(((row_end - row0 - 1) * m + sw) * s);
+    const T* gbase = static_cast<const T*>(a.grads[d.tensor]) + row0 * m + j_begin;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(gbase), 0, int(nrec), 0x00020000);
+
+    float x[kOddSlots][4];
+    float at[QN][KC][RC];
+    auto issue = [&](int rb0) {
+        if constexpr (K > 0) {  // error-feedback rows P_k[i][cq + 4b] (clamped, pinned later)
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                const int64_t i = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16) + ri;
+                const int64_t ic = i < row_end ? i : row0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+#pragma unroll
+                    for (int bb = 0; bb < RC; ++bb) {
+                        const int c = cq + 4 * bb;
+                        at[q][k][bb] = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
+                    }
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < kOddSlots; ++sl) {
+            const int q = sl / KN, ks = sl % KN;
+            const uint32_t roff = uint32_t((wave * 16 + (rb0 + q) * (kWaves * 16) + ri) * int64_t(m)) * s;
+            const int32_t jj = ks * 16 + 4 * cq;
+            if constexpr (VEC) {
+                BufIo<T>::ld4(rs, jj < sw ? roff + uint32_t(jj) * s : kOob, x[sl]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    x[sl][e] = BufIo<T>::ld1(rs, jj + e < sw ? roff + uint32_t(jj + e) * s : kOob);
+            }
+        }
+    };
+
+    auto process = [&](int rb0) {
+        f32x4_t acc[QN];
+#pragma unroll
+        for (int q = 0; q < QN; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                const bool rv = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16) + ri < row_end;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+#pragma unroll
+                    for (int bb = 0; bb < RC; ++bb) {
+                        keep(at[q][k][bb]);
+                        at[q][k][bb] = (rv && cq + 4 * bb < r) ? at[q][k][bb] : 0.f;
+                    }
+            }
+        }
+#pragma unroll
+        for (int sl = 0; sl < kOddSlots; ++sl) {
+            const int q = sl / KN, ks = sl % KN;
+            if (ks < nks) {  // wave-uniform; the loads were all issued before
+                const int32_t js = ks * 16;
+                const int32_t jj = js + 4 * cq;
+                if constexpr (K > 0) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int bb = 0; bb < RC; ++bb) {
+                            const int c = cq + 4 * bb;
+                            const int32_t jr = js + ri;
+                            const bool ok = jr < sw && c < r;
+                            const float av = bs[(k * kOddSW + (jr < sw ? jr : 0)) * RP + c];
+                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, at[q][k][bb], corr, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[sl][e] -= corr[e];
+                    }
+                } else {
+                    const int64_t i = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16) + ri;
+                    const bool rv = i < row_end;
+                    const int64_t ic = rv ? i : row0;
+                    for (int k = 0; k < nt; ++k) {  // many terms: panels straight from L1/L2
+                        const gptr<const float> Bq = gconst<float>(a.res.q[k]) + d.qoff;
+                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int bb = 0; bb < RC; ++bb) {
+                            const int c = cq + 4 * bb;
+                            const int32_t jr = js + ri;
+                            const bool ok = jr < sw && c < r;
+                            const float av = Bq[int64_t(j_begin + (ok ? jr : 0)) * r + (ok ? c : 0)];
+                            const float pv = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
+                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, (rv && c < r) ? pv : 0.f,
+                                                                        corr, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[sl][e] -= corr[e];
+                    }
+                }
+                // xt rows are zero-padded to a multiple of 4 columns: one aligned 16-byte read
+                const v4f bx4 = *reinterpret_cast<const v4f*>(xt + cx * kOddXT + (jj < sw ? jj : 0));
+                const bool okx = cvalid && jj < sw;
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][0], okx ? bx4.x : 0.f, acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][1], okx ? bx4.y : 0.f, acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][2], okx ? bx4.z : 0.f, acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][3], okx ? bx4.w : 0.f, acc[q], 0, 0, 0);
+            }
+        }
+        // acc[q][e] = partial P[i0 + 4 cq + e][c = ri] of row block rb0 + q
+        if (cvalid) {
+            gptr<float> part = gmut<float>(a.part) + d.part_odd + int64_t(t.strip) * n * r;
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                const int64_t i0 = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t ii = i0 + 4 * cq + e;
+                    if (ii < row_end) part[ii * r + ri] = acc[q][e];
+                }
+            }
+        }
+    };
+
+    issue(0);  // in flight while the strips are staged
 
     // Stage the strip's factor panels once per tile: xt[c][j] = X[j_begin + j][c]
     // (transposed: a lane's four B-operands of one k-step are one ds_read_b128) and
@@ -402,108 +754,10 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
         __syncthreads();
     }
 
-    for (int64_t i0 = row0 + wave * 16; i0 < row_end; i0 += kWaves * 16) {
-        const int64_t i = i0 + ri;
-        const bool rv = i < row_end;
-        const int64_t ic = rv ? i : row0;
-        const gptr<const T> Grow = G + ic * m;
-        float at[KC][RC];
-#pragma unroll
-        for (int k = 0; k < KC; ++k)
-#pragma unroll
-            for (int b = 0; b < RC; ++b) at[k][b] = 0.f;
-        if constexpr (K > 0) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-#pragma unroll
-                for (int b = 0; b < RC; ++b) {
-                    const int c = cq + 4 * b;
-                    const float v = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
-                    at[k][b] = (rv && c < r) ? v : 0.f;
-                }
-        }
-        f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-        for (int32_t j0 = 0; j0 < sw; j0 += 16 * U) {
-            float x[U][4];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t jj = j0 + 16 * u + 4 * cq;
-                if constexpr (VEC) {  // sw % 4 == 0: the four columns are valid together
-                    Io<T>::ld(Grow + j_begin + (jj < sw ? jj : 0), x[u]);
-                } else {              // any m: four element loads, each clamped
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        float v1[1];
-                        Io<T>::ld(Grow + j_begin + (jj + e < sw ? jj + e : 0), v1);
-                        x[u][e] = v1[0];
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t jj = j0 + 16 * u + 4 * cq;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    keep(x[u][e]);
-                    x[u][e] = (rv && jj + (VEC ? 0 : e) < sw) ? x[u][e] : 0.f;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t js = j0 + 16 * u;
-                if (js >= sw) break;  // wave-uniform
-                if constexpr (K > 0) {
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int b = 0; b < RC; ++b) {
-                            const int c = cq + 4 * b;
-                            const int32_t jr = js + ri;
-                            const bool ok = jr < sw && c < r;
-                            const float av = bs[(k * kOddSW + (jr < sw ? jr : 0)) * RP + c];
-                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, at[k][b], corr, 0, 0, 0);
-                        }
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) x[u][e] -= corr[e];
-                    }
-                } else {
-                    for (int k = 0; k < nt; ++k) {  // many terms: panels straight from L1/L2
-                        const gptr<const float> Bq = gconst<float>(a.res.q[k]) + d.qoff;
-                        f32x4_t corr = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int b = 0; b < RC; ++b) {
-                            const int c = cq + 4 * b;
-                            const int32_t jr = js + ri;
-                            const bool ok = jr < sw && c < r;
-                            const float av = Bq[int64_t(j_begin + (ok ? jr : 0)) * r + (ok ? c : 0)];
-                            const float pv = gconst<float>(a.res.p[k])[d.poff + ic * r + (c < r ? c : 0)];
-                            corr = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? av : 0.f, (rv && c < r) ? pv : 0.f,
-                                                                        corr, 0, 0, 0);
-                        }
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) x[u][e] -= corr[e];
-                    }
-                }
-                const int32_t jq = js + 4 * cq;
-                // xt rows are zero-padded to a multiple of 4 columns: one aligned 16-byte read
-                const v4f bx4 = *reinterpret_cast<const v4f*>(xt + cx * kOddXT + (jq < sw ? jq : 0));
-                const bool okx = cvalid && jq < sw;
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][0], okx ? bx4.x : 0.f, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][1], okx ? bx4.y : 0.f, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][2], okx ? bx4.z : 0.f, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][3], okx ? bx4.w : 0.f, acc, 0, 0, 0);
-            }
-        }
-        // acc[e] = partial P[i0 + 4 cq + e][c = ri]
-        if (cvalid) {
-            gptr<float> part = gmut<float>(a.part) + d.part_odd + int64_t(t.strip) * n * r;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t ii = i0 + 4 * cq + e;
-                if (ii < row_end) part[ii * r + ri] = acc[e];
-            }
-        }
+    if (nrb > 0) process(0);
+    for (int rb0 = QN; rb0 < nrb; rb0 += QN) {
+        issue(rb0);
+        process(rb0);
     }
 }
 
@@ -513,10 +767,14 @@ __global__ __launch_bounds__(kBlock) void k_odd_mfma(ProductArgs a) {
     __shared__ __attribute__((aligned(16))) float bs[(K > 0 ? K : 1) * kOddSW * 4 * RC];
     const Tile t = a.tiles[blockIdx.x];
     const MatDesc d = a.mats[t.mat];
-    if (d.vec)
-        odd_mfma_tile<T, 1, RC, K>(a, d, t, xt, bs);
-    else
-        odd_mfma_tile<T, 0, RC, K>(a, d, t, xt, bs);
+    const bool wide = d.odd_sw > 64;
+    if (d.vec) {
+        if (wide) odd_mfma_tile<T, 1, RC, K, true>(a, d, t, xt, bs);
+        else odd_mfma_tile<T, 1, RC, K, false>(a, d, t, xt, bs);
+    } else {
+        if (wide) odd_mfma_tile<T, 0, RC, K, true>(a, d, t, xt, bs);
+        else odd_mfma_tile<T, 0, RC, K, false>(a, d, t, xt, bs);
+    }
 }
 
 template <typename T>
