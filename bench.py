@@ -9,8 +9,10 @@ N > 1: one process per GPU (torch.distributed.run), every rank holds its own gra
 (data parallel, weak scaling) and the P/Q factors are SUM-all-reduced over RCCL.
 
 Prints ONE JSON line on rank 0. ``value`` = gradient bytes processed by all ranks per
-second (GB/s). ``roofline`` = the fused residual/output kernel (k_apply, the dominant
-kernel), timed with HIP events on the launch stream over the timed region.
+second (GB/s). ``roofline`` = the final pass, the dominant kernel: k_final_odd (the last
+odd power iteration fused with the residual/output writes) or k_apply (residual + output
+after an even last iteration), timed with HIP events on the launch stream over the timed
+region.
 ``cpu_baseline`` = the CPU oracle (bit-identical restatement of the reference) on a
 bounded sample, rank 0 at N = 1 only.
 """
@@ -52,11 +54,14 @@ def numel(s):
     return n
 
 
-def apply_alg_bytes(c, mask, world):
-    """Algorithmic HBM bytes of ONE k_apply launch: read G0, write residual, write output
-    (s bytes each per element) + the factor panels it must read (fp32)."""
+def apply_alg_bytes(c, mask, world, fused):
+    """Algorithmic HBM bytes of ONE final-pass launch + the factor panels it must read (fp32).
+    k_apply: read G0, write residual, write output (s bytes each per element).
+    k_final_odd (fused last odd iteration): read G0, write residual, and at world size 1
+    write the output (2 or 3 s bytes per element)."""
     s = 2 if c["dtype"] == "bf16" else 4
     terms = 1 if world == 1 else 2
+    per = 3 if (not fused or world == 1) else 2
     total = 0
     for shp, comp in zip(c["shapes"], mask):
         if not comp:
@@ -64,13 +69,15 @@ def apply_alg_bytes(c, mask, world):
         n = shp[0]
         m = numel(shp) // n
         r = min(c["rank"], n, m)
-        total += 3 * s * n * m + 4 * terms * c["iters"] * r * (n + m)
+        total += per * s * n * m + 4 * terms * c["iters"] * r * (n + m)
     return total
 
 
-def step_alg_bytes(c, mask, world):
-    """sum_c s*n*m*(I+3) + sum_c 4*I*r*(n+m) + sum_u 3*s*N."""
+def step_alg_bytes(c, mask, world, fused):
+    """sum_c s*n*m*(I+3) + sum_c 4*I*r*(n+m) + sum_u 3*s*N. With the fused
+    last odd iteration the gradient is read once less: (I+2) instead of (I+3)."""
     s = 2 if c["dtype"] == "bf16" else 4
+    passes = c["iters"] + (2 if fused else 3)
     total = 0
     for shp, comp in zip(c["shapes"], mask):
         N = numel(shp)
@@ -78,7 +85,7 @@ def step_alg_bytes(c, mask, world):
             n = shp[0]
             m = N // n
             r = min(c["rank"], n, m)
-            total += s * N * (c["iters"] + 3) + 4 * c["iters"] * r * (n + m)
+            total += s * N * passes + 4 * c["iters"] * r * (n + m)
         else:
             total += 3 * s * N
     return total
@@ -166,7 +173,15 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     value = world * grad_bytes * a.steps / elapsed / 1e9
     mask = psgd.is_compressed_mask
-    ab = apply_alg_bytes(c, mask, world)
+    # which final pass each timed step took (I odd: steps alternate between the fused last odd
+    # iteration and k_apply); bytes are averaged over the timed steps
+    first = codec.step_counter - a.steps
+    nf = sum(codec._plan.fused_final(t) for t in range(first, codec.step_counter))
+    frac_f = nf / a.steps
+    ab = frac_f * apply_alg_bytes(c, mask, world, True) + (1 - frac_f) * apply_alg_bytes(c, mask, world, False)
+    sb = frac_f * step_alg_bytes(c, mask, world, True) + (1 - frac_f) * step_alg_bytes(c, mask, world, False)
+    kf = "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")")
+    kname = kf if nf == a.steps else "k_apply (fused residual + output)" if nf == 0 else f"{kf} / k_apply, alternating"
     achieved = ab / (apply_ms * 1e-3) / 1e9
     out = {
         "metric": "gradient GB/s compressed+decompressed (device-resident)",
@@ -185,13 +200,13 @@ def main():
                    "min_compression_rate": c["mcr"], "tensors": len(shapes),
                    "compressed_tensors": sum(mask), "gradient_bytes_per_rank": grad_bytes,
                    "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "k_apply (fused residual + output)", "bound": "hbm",
+        "roofline": {"kernel": kname, "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(a.config),
-                     "alg_bytes_per_launch": ab, "avg_launch_us": round(apply_ms * 1e3, 2)},
-        "step_roofline": {"alg_bytes_per_step": step_alg_bytes(c, mask, world),
-                          "achieved_GBs": round(step_alg_bytes(c, mask, world) / (ms_step * 1e-3) / 1e9, 1),
-                          "frac": round(step_alg_bytes(c, mask, world) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                     "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2)},
+        "step_roofline": {"alg_bytes_per_step": round(sb),
+                          "achieved_GBs": round(sb / (ms_step * 1e-3) / 1e9, 1),
+                          "frac": round(sb / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)

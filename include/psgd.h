@@ -11,6 +11,7 @@
  *                          (orthogonalize :188 -> orthogonalization.py:4-8; bmm :189-193;
  *                           local error-feedback update :195-202)
  *   psgd_decompress        approximation + un-batching  powersgd/powersgd.py:211-230
+ *   psgd_plan_fused_final  (which final-pass form a step takes; no reference counterpart)
  *   psgd_aggregate         BasicPowerSGD.aggregate      powersgd/powersgd.py:146-235 (world size 1)
  *   psgd_flat_*            AllReduce.aggregate          powersgd/powersgd.py:22-31,
  *                          pack / allreduce_average      powersgd/utils.py:6-10, :43-49
@@ -104,8 +105,12 @@ int psgd_out_factor(const psgd_plan* plan, int64_t step, int32_t it, int32_t* wh
 /* One power iteration on every compressed matrix: orthonormalise the in-factor (rank 1:
  * one joint norm per shape group; rank > 1: Householder QR per matrix), then the
  * tall-skinny product with the error-feedback matrix G_it = G_0 - sum_{j<it} P_j Q_j^T
- * (formed on the fly, gradients are not written). Leaves the LOCAL factor in the out-
- * factor state buffer. `grads[i]` = device pointer of compressed tensor i (contiguous). */
+ * (formed on the fly). Leaves the LOCAL factor in the out-factor state buffer.
+ * `grads[i]` = device pointer of compressed tensor i (contiguous).
+ * Gradients are not written, EXCEPT by the last iteration of a step for which
+ * psgd_plan_fused_final() reports 1: that iteration (odd, P = G X) is fused with the
+ * final pass and leaves the error-feedback residual in `grads` (reference :195-202, :230);
+ * psgd_decompress then only writes the output. */
 int psgd_compress(psgd_plan* plan, void* const* grads, int64_t step, int32_t it, void* stream);
 
 /* Fused final pass: grads[i] <- G_0 - sum_k P_k Q_k^T (local factors) and
@@ -118,8 +123,13 @@ int psgd_decompress(psgd_plan* plan, void* const* grads, void* out, int64_t step
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);
 
-/* Kernel timing for benchmarks: when enabled, every fused final pass (k_apply) launched by
- * psgd_decompress/psgd_aggregate is bracketed by HIP events recorded on its own stream.
+/* 1 when the last iteration of `step` is odd and every matrix fits the fused final pass
+ * (row-resident product + residual, psgd_final.cuh): psgd_compress of that iteration then
+ * writes the residual. */
+int psgd_plan_fused_final(const psgd_plan* plan, int64_t step, int32_t* fused);
+
+/* Kernel timing for benchmarks: when enabled, every final pass launched by psgd_aggregate
+ * (k_apply, or the fused final odd kernel) and by psgd_decompress (k_apply) is bracketed by HIP events recorded on its own stream.
  * psgd_plan_timing_read waits for the recorded events, returns the summed kernel time (ms)
  * and the number of launches, and clears the record. */
 int psgd_plan_set_timing(psgd_plan* plan, int32_t enable);

@@ -36,6 +36,7 @@ _SIGNATURES = {
     "psgd_compress": ([_vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_decompress": ([_vp, _vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_aggregate": ([_vp, _vp, _vp, _i64, _vp], _i32),
+    "psgd_plan_fused_final": ([_vp, _i64, _P_i32], _i32),
     "psgd_plan_set_timing": ([_vp, _i32], _i32),
     "psgd_plan_timing_read": ([_vp, _P_dbl, _P_i32], _i32),
     "psgd_flat_create": ([_P_i64, _i32, _i32, ctypes.POINTER(_vp)], _i32),
@@ -168,6 +169,12 @@ class Plan:
 
     def aggregate(self, grads, out_ptr: int, step: int, stream: int) -> None:
         check(lib().psgd_aggregate(self._h, grads, out_ptr, step, stream))
+
+    def fused_final(self, step: int) -> bool:
+        """True when the last iteration of ``step`` runs fused with the final pass."""
+        f = _i32()
+        check(lib().psgd_plan_fused_final(self._h, step, ctypes.byref(f)))
+        return bool(f.value)
 
     def set_timing(self, enable: bool) -> None:
         check(lib().psgd_plan_set_timing(self._h, 1 if enable else 0))

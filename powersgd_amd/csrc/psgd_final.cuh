@@ -1,0 +1,422 @@
+// Final-pass kernels (gfx950, wave64).
+//
+// k_final_odd — the LAST power iteration when it is odd (P = G_k X, reference
+// powersgd.py:185-202 with the transposed views) fused with the final pass (:195-230).
+// A row group of T threads (T = 4..64 lanes of one wave, or 2 / 4 whole waves) owns one
+// gradient row at a time: thread t holds columns 4 (s T + t) .. +3 of segments s < S in
+// registers, so
+//   1. g = G_0[i, :] - sum_{j<k} P_j[i] Q_j^T        (error feedback, formed on the fly)
+//   2. P[i, :] = g . X                                 (thread dots + DPP / LDS row sum)
+//   3. residual[i, :] = g - P[i] X^T                   (from the same registers)
+//      output[i, :]   = sum_{j<=k} P_j[i] Q_j^T        (world size 1 only)
+// The gradient is read ONCE for the last iteration and its finalisation together: the
+// separate odd product + partial reduction + k_apply read it twice and ran three launches.
+// The factor panels of a row group's columns (X and the earlier terms' Q_j) stay in
+// registers for all rows of the workgroup's row block.
+//
+// k_lowrank_out — output = alpha * sum_k Pbar_k Qbar_k^T for world size > 1 after a fused
+// final iteration (the all-reduced factor of the last iteration is only known after the
+// collective, :204-219): writes the output, reads no gradient.
+#pragma once
+
+#include "psgd_stream.cuh"
+
+namespace psgd {
+
+// Rows per row group per batch: 4 at rank 1 (more bytes in flight per wave), 2 above.
+template <int R>
+struct FinRB {
+    static constexpr int value = R == 1 ? 4 : 2;
+};
+
+// Gradient / output rows go through buffer descriptors spanning exactly one matrix: a
+// slot past the row end or past the matrix gets offset kOob, which loads 0 and drops the
+// store in hardware (no clamping, no branches). The plan keeps a fused matrix below 2^31
+// bytes.
+template <typename T>
+struct FinIo;
+
+template <>
+struct FinIo<float> {
+    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+    }
+    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+    }
+};
+
+template <>
+struct FinIo<bf16_t> {
+    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
+        typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
+        const v2u_ x = {uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                        uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+    }
+    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, 0);
+    }
+};
+
+// Four consecutive row elements [c, c+4) at element offset `e` (= row * m + c): one vector
+// access with the vector layout (m % 4 == 0, aligned), else four scalar accesses.
+template <typename T, bool VEC>
+__device__ __forceinline__ void fin_ld(rsrc_t rs, uint32_t e, bool ok, int32_t c, int32_t m, float (&v)[4]) {
+    constexpr uint32_t s = sizeof(T);
+    if constexpr (VEC) {
+        BufIo<T>::ld4(rs, ok ? e * s : kOob, v);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = BufIo<T>::ld1(rs, (ok && c + q < m) ? (e + q) * s : kOob);
+    }
+}
+template <typename T, bool VEC>
+__device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c, int32_t m, const float (&v)[4]) {
+    constexpr uint32_t s = sizeof(T);
+    if constexpr (VEC) {
+        FinIo<T>::st4(rs, ok ? e * s : kOob, v);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) FinIo<T>::st1(rs, (ok && c + q < m) ? (e + q) * s : kOob, v[q]);
+    }
+}
+
+template <typename T, int R, int K, int SMAX, bool VEC>
+__device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
+                                               float (*red)[kWaves][FinRB<R>::value * R]) {
+    constexpr int RB = FinRB<R>::value;
+    constexpr int KC = K > 0 ? K : 1;
+    const int r = d.r;
+    const int32_t m = int32_t(d.m);
+    const int Tg = d.fin_T, S = d.fin_S;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = tid / Tg, tt = tid - rg * Tg;
+    const int RGS = kBlock / Tg;
+    const int64_t row0 = int64_t(t.chunk) * d.fin_rows;
+    const int64_t row_end = d.n < row0 + d.fin_rows ? d.n : row0 + d.fin_rows;
+    const int nres = K >= 0 ? K : a.nres;
+    const uint32_t nbytes = uint32_t(d.n * d.m * int64_t(sizeof(T)));
+    const rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.grads[d.tensor], 0, int(nbytes), 0x00020000);
+    const rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(static_cast<T*>(a.out) + d.out_off, 0, int(nbytes),
+                                                        0x00020000);
+    const gptr<const float> X = gconst<float>(a.x) + d.qoff;
+
+    // rank-1 joint norm of the raw in-factor (world size 1, fused): x / max(||x||, eps)
+    const bool norm = a.ss_in != nullptr;
+    const float dn = norm ? group_norm_ss(a.ss_in, a.grng_in, d.group) : 1.f;
+    if (norm && t.chunk == 0) {  // row block 0 publishes this matrix's normalised in-factor
+        for (int64_t e = tid; e < d.m * r; e += kBlock) {
+            const float v = X[e] / dn;
+            a.xstate[d.qoff + e] = v;
+            a.hx[d.qoff + e] = v;
+        }
+    }
+
+    int32_t ccol[SMAX];
+    bool act[SMAX];
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+        const int32_t c = (s * Tg + tt) * 4;
+        act[s] = s < S && c < m;
+        ccol[s] = act[s] ? c : 0;
+    }
+    // factor row of column c (clamped to column 0 past the end of a ragged row)
+    auto fcol = [&](int s, int v) { return ccol[s] + v < m ? ccol[s] + v : 0; };
+    float xq[SMAX][4][R];
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+        if (s < S) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                ld_factor<R>(X + fcol(s, v) * r, r, xq[s][v]);
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
+                    xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
+                }
+            }
+        }
+    }
+    float bq[KC][SMAX][4][R];
+    if constexpr (K > 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s)
+                if (s < S) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, bq[k][s][v]);
+                }
+    }
+
+    const int64_t rows = row_end - row0;
+    const int nb = int((rows + int64_t(RGS) * RB - 1) / (int64_t(RGS) * RB));
+    for (int b = 0; b < nb; ++b) {
+        const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
+        int64_t ic[RB];
+        float g[RB][SMAX][4];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            ic[u] = ib + u < row_end ? ib + u : row0;  // factor rows: clamped, in range
+            const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s)
+                if (s < S) fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, g[u][s]);
+        }
+        float ap[KC][RB][R];
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int u = 0; u < RB; ++u)
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic[u] * r, r, ap[k][u]);
+        }
+        float dot[RB][R];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s)
+                if (s < S) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) keep(g[u][s][v]);
+                }
+#pragma unroll
+            for (int c = 0; c < R; ++c) dot[u][c] = 0.f;
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+                if (s < S) {
+                    // error feedback of the earlier iterations (reference :195-202), same
+                    // per-element arithmetic as the product and k_apply
+                    if constexpr (K > 0) {
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) g[u][s][v] = g[u][s][v] - dotr<R>(ap[k][u], bq[k][s][v]);
+                    } else if constexpr (K < 0) {
+                        for (int k = 0; k < nres; ++k) {
+                            float pa[R];
+                            ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic[u] * r, r, pa);
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) {
+                                float qb[R];
+                                ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, qb);
+                                g[u][s][v] = g[u][s][v] - dotr<R>(pa, qb);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+#pragma unroll
+                        for (int c = 0; c < R; ++c) dot[u][c] = fmaf(g[u][s][v], xq[s][v][c], dot[u][c]);
+                }
+            }
+        }
+        // row sums over the T threads of the row group (fixed order: DPP tree, then waves
+        // in index order)
+        if (Tg <= 64) {
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+                for (int c = 0; c < R; ++c) dot[u][c] = sum_within(dot[u][c], Tg);
+        } else {
+            float* buf = &red[b & 1][0][0];
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    dot[u][c] = wave_allsum(dot[u][c]);
+                    if (lane == 0) buf[wave * RB * R + u * R + c] = dot[u][c];
+                }
+            __syncthreads();
+            const int w0 = rg * (Tg >> 6), nw = Tg >> 6;
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    float sum = buf[w0 * RB * R + u * R + c];
+                    for (int w = 1; w < nw; ++w) sum += buf[(w0 + w) * RB * R + u * R + c];
+                    dot[u][c] = sum;
+                }
+        }
+        // the local out-factor rows (history + the reference-visible P state, :189-193)
+        if (tt == 0) {
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+                if (ib + u < row_end) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c)
+                        if (c < r) {
+                            const int64_t e = d.poff + (ib + u) * r + c;
+                            a.yloc[e] = dot[u][c];
+                            a.state[e] = dot[u][c];
+                        }
+                }
+        }
+        // residual (and output at world size 1) from the registers
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            float pr[R];
+#pragma unroll
+            for (int c = 0; c < R; ++c) pr[c] = c < r ? dot[u][c] : 0.f;
+            const bool valid = ib + u < row_end;
+            const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s) {
+                if (s < S) {
+                    float res[4], o[4];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const float tl = dotr<R>(pr, xq[s][v]);
+                        res[v] = g[u][s][v] - tl;
+                        if (a.write_out) {
+                            float acc = 0.f;
+                            if constexpr (K > 0) {
+#pragma unroll
+                                for (int k = 0; k < K; ++k) acc = acc + dotr<R>(ap[k][u], bq[k][s][v]);
+                            } else if constexpr (K < 0) {
+                                for (int k = 0; k < nres; ++k) {
+                                    float pa[R], qb[R];
+                                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic[u] * r, r, pa);
+                                    ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, qb);
+                                    acc = acc + dotr<R>(pa, qb);
+                                }
+                            }
+                            o[v] = acc + tl;
+                        }
+                    }
+                    const bool ok = valid && act[s];
+                    fin_st<T, VEC>(gs, rowe + uint32_t(ccol[s]), ok, ccol[s], m, res);
+                    if (a.write_out) fin_st<T, VEC>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int R, int K, int SMAX>
+__global__ __launch_bounds__(kBlock) void k_final_odd(FinalArgs a) {
+    __shared__ float red[2][kWaves][FinRB<R>::value * R];
+    const Tile t = a.tiles[blockIdx.x];
+    const MatDesc d = a.mats[t.mat];
+    if (d.vec)
+        final_odd_tile<T, R, K, SMAX, true>(a, d, t, red);
+    else
+        final_odd_tile<T, R, K, SMAX, false>(a, d, t, red);
+}
+
+// output = sum_k alpha * (A_k B_k^T) on the lane-column tiles (same order as k_apply's
+// output term, reference :211-219)
+template <typename T, int R, int NI, int V>
+__device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
+    const TileGeom g = tile_geom<V>(d, t);
+    const int r = d.r;
+    const gptr<T> O = gmut<T>(a.out) + d.out_off;
+    const int nt = NI > 0 ? NI : a.nterms;
+    constexpr int NC = NI > 0 ? NI : 1;
+    float ba[NC][V][R];
+    if constexpr (NI > 0) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                ld_factor<R>(gconst<float>(a.apx.q[k]) + d.qoff + (g.ccol + v) * r, r, ba[k][v]);
+    }
+    const float alpha = a.alpha;
+    for (int64_t row = g.first_row; row < g.row_end; row += g.stride) {
+        const int32_t prow = int32_t(row) * r;
+        float o[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) o[v] = 0.f;
+        for (int k = 0; k < nt; ++k) {
+            float aa[R];
+            ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, aa);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                float bb[R];
+                if constexpr (NI > 0) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c) bb[c] = ba[k < NC ? k : 0][v][c];
+                } else {
+                    ld_factor<R>(gconst<float>(a.apx.q[k]) + d.qoff + (g.ccol + v) * r, r, bb);
+                }
+                o[v] = o[v] + alpha * dotr<R>(aa, bb);
+            }
+        }
+        if (g.active) Io<T>::st(O + int64_t(row) * g.m + g.col0, o);
+    }
+}
+
+template <typename T, int R, int NI>
+__global__ __launch_bounds__(kBlock) void k_lowrank_out(ApplyArgs a) {
+    const Tile t = a.tiles[blockIdx.x];
+    const MatDesc d = a.mats[t.mat];
+    if constexpr (R <= 8) {
+        if (d.vec) {
+            lowrank_tile<T, R, NI, 4>(a, d, t);
+            return;
+        }
+    }
+    lowrank_tile<T, R, NI, 1>(a, d, t);
+}
+
+// ------------------------------------------------------------------ dispatch ------
+// SMAX (register segments) is the smallest instantiated bucket >= the plan's max fin_S.
+template <typename T, int R, int SMAX>
+hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s) {
+    const dim3 grid(ntiles), block(kBlock);
+    switch (nres) {
+        case 0: k_final_odd<T, R, 0, SMAX><<<grid, block, 0, s>>>(a); break;
+        case 1: k_final_odd<T, R, 1, SMAX><<<grid, block, 0, s>>>(a); break;
+        default: k_final_odd<T, R, -1, SMAX><<<grid, block, 0, s>>>(a); break;
+    }
+    return hipGetLastError();
+}
+
+template <typename T, int R>
+hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s) {
+    if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s);
+    if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s);
+    if (smax <= 12) return dispatch_final_k<T, R, 12>(nres, a, ntiles, s);
+    return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t dispatch_final(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s) {
+    switch (R) {
+        case 1: return dispatch_final_r<T, 1>(nres, smax, a, ntiles, s);
+        case 2: return dispatch_final_r<T, 2>(nres, smax, a, ntiles, s);
+        case 4: return dispatch_final_r<T, 4>(nres, smax, a, ntiles, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename T, int R>
+hipError_t dispatch_lowrank_r(int nterms, const ApplyArgs& a, int ntiles, hipStream_t s) {
+    const dim3 grid(ntiles), block(kBlock);
+    switch (R <= 8 ? nterms : -1) {
+        case 1: k_lowrank_out<T, R, 1><<<grid, block, 0, s>>>(a); break;
+        case 2: k_lowrank_out<T, R, 2><<<grid, block, 0, s>>>(a); break;
+        case 4: k_lowrank_out<T, R, 4><<<grid, block, 0, s>>>(a); break;
+        default: k_lowrank_out<T, R, -1><<<grid, block, 0, s>>>(a); break;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch_lowrank(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s) {
+    switch (R) {
+        case 1: return dispatch_lowrank_r<T, 1>(nterms, a, ntiles, s);
+        case 2: return dispatch_lowrank_r<T, 2>(nterms, a, ntiles, s);
+        case 4: return dispatch_lowrank_r<T, 4>(nterms, a, ntiles, s);
+        case 8: return dispatch_lowrank_r<T, 8>(nterms, a, ntiles, s);
+        case 16: return dispatch_lowrank_r<T, 16>(nterms, a, ntiles, s);
+        case 32: return dispatch_lowrank_r<T, 32>(nterms, a, ntiles, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace psgd

@@ -31,6 +31,12 @@ struct MatDesc {
     int32_t odd_nstrip;     // column strips of the odd partials (reduce pass)
     int32_t odd_sw;         // MFMA strip width (columns, multiple of 16)
     int32_t odd_chunk_rows; // MFMA chunk rows (multiple of 16 * kWaves)
+    // fused final odd iteration (k_final_odd): a row group of fin_T threads owns a row
+    // (fin_S segments of 4*fin_T columns); a workgroup covers fin_rows rows
+    int32_t fin_T;
+    int32_t fin_S;
+    int32_t fin_rows;
+    int32_t fin_pad;
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
@@ -104,6 +110,27 @@ struct ReduceArgs {
     float* ss_out;       // per-item sum of squares of this reduction's output (or null)
 };
 
+// Fused LAST iteration when it is odd (P = G_k X): a row group holds whole rows in
+// registers, so the reduction over columns completes inside the workgroup and the same
+// registers produce the residual (and, at world size 1, the output) without re-reading G.
+struct FinalArgs {
+    const MatDesc* mats;
+    const Tile* tiles;    // (mat, 0, row block)
+    void* const* grads;   // in: G_0, out: residual
+    void* out;            // flat output (written when write_out)
+    const float* x;       // in-factor, Q layout (orthonormal, or raw when ss_in is set)
+    Terms res;            // local terms of the earlier iterations (also the output terms at W = 1)
+    int32_t nres;
+    int32_t write_out;    // world size 1: output = sum of all terms
+    float* yloc;          // P local -> history
+    float* state;         // P local -> reference-visible state buffer
+    // rank-1 fused normalisation of the raw in-factor (as ReduceArgs)
+    const float* ss_in;
+    const int32_t* grng_in;
+    float* xstate;
+    float* hx;
+};
+
 struct OrthArgs {
     const OrthUnit* units;
     float* state;        // in-factor state buffer, orthonormalised in place
@@ -140,6 +167,9 @@ hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int
                            hipStream_t s);
 hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a,
                         int ntiles, hipStream_t s);
+hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
+                            hipStream_t s);
+hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);

@@ -29,6 +29,21 @@ hipError_t launch_apply_bf16(int R, int nterms, bool shared, const ApplyArgs& a,
 hipError_t launch_odd_mfma_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_odd_mfma_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 
+hipError_t launch_final_odd_f32(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_lowrank_out_f32(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_lowrank_out_bf16(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
+
+hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
+                            hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_final_odd_f32(R, nres, smax, a, ntiles, s)
+                             : launch_final_odd_bf16(R, nres, smax, a, ntiles, s);
+}
+hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_lowrank_out_f32(R, nterms, a, ntiles, s)
+                             : launch_lowrank_out_bf16(R, nterms, a, ntiles, s);
+}
+
 hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     return dtype == PSGD_F32 ? launch_odd_mfma_f32(R, nres, a, ntiles, s)
                              : launch_odd_mfma_bf16(R, nres, a, ntiles, s);
@@ -125,6 +140,39 @@ OddGeom odd_geometry(int64_t n, int64_t m, int64_t tile_elems) {
     return g;
 }
 
+struct FinGeom {
+    int T, S, rows;
+    int64_t ntiles;
+};
+
+// Fused final odd pass (psgd_final.cuh): row groups of T threads (4 columns each, S
+// segments), fin_rb(R) rows per group per batch, blocks of about fin_elems elements.
+int fin_rb(int R) { return R == 1 ? 4 : 2; }  // == FinRB<R>
+FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems) {
+    FinGeom g;
+    const int64_t q4 = (m + 3) / 4;
+    g.T = int(std::min<int64_t>(kBlock, pow2ceil(q4)));
+    g.S = int((q4 + g.T - 1) / g.T);
+    const int64_t batch = int64_t(kBlock / g.T) * fin_rb(R);  // rows per workgroup batch
+    int64_t rows = round_up(std::max<int64_t>(1, (fin_elems + m - 1) / m), batch);
+    // a small matrix must still spread over several workgroups
+    rows = std::min(rows, std::max(batch, round_up((n + 7) / 8, batch)));
+    rows = std::min(rows, round_up(n, batch));
+    g.rows = int(rows);
+    g.ntiles = (n + rows - 1) / rows;
+    return g;
+}
+
+// VGPR estimate of the fused kernel (cached factor panels + row data + term rows + ~40
+// of addressing and temporaries; calibrated against -Rpass-analysis=kernel-resource-usage,
+// tools/regs.py). Above 200 the kernel drops to one wave per SIMD, so the plan keeps the
+// unfused final iteration instead.
+int fin_regs(int R, int smax, int nres) {
+    const int panels = 1 + (nres == 1 ? 1 : 0);
+    return smax * 4 * R * panels + fin_rb(R) * smax * 4 + 8 * R * fin_rb(R) + 40;
+}
+int fin_bucket(int s) { return s <= 2 ? 2 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
+
 struct DevScope {  // make `dev` current for the scope, restore afterwards
     int prev = -1;
     explicit DevScope(int dev) {
@@ -160,6 +208,10 @@ struct psgd_plan {
     std::vector<Tile> tiles;     // lane-column tiles of every matrix (even products, apply)
     std::vector<Tile> tiles_ov;  // lane-column tiles of the odd-VALU matrices
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
+    std::vector<Tile> tiles_fin; // row blocks of the fused final odd pass
+    bool fin_ok = false;         // every matrix fits the fused final odd pass
+    int fin_smax = 0;
+    int64_t fin_elems = 32768, tiles_fin_cap = 0;
     int64_t tiles_cap = 0, tiles_om_cap = 0;
     std::vector<RedItem> red_even, red_odd;
     std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
@@ -167,7 +219,7 @@ struct psgd_plan {
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_floats = 0;
     double unc_floats = 0, comp_floats = 0;
-    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_red_even = 0,
+    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_tiles_fin = 0, o_red_even = 0,
            o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, o_grng_even = 0,
            o_grng_odd = 0, o_ss = 0, ss_stride = 0, ws_bytes = 0;
     bool bound = false;
@@ -176,6 +228,7 @@ struct psgd_plan {
     float* Q = nullptr;
     char* ws = nullptr;
     std::vector<void*> host_ptrs;
+    void* out_now = nullptr;  // psgd_aggregate's output buffer (fused final pass)
     // benchmark timing of k_apply: event pairs recorded on the launch stream
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -200,6 +253,9 @@ struct psgd_plan {
         tiles.clear();
         tiles_ov.clear();
         tiles_om.clear();
+        tiles_fin.clear();
+        fin_ok = env_int("PSGD_FUSE_FINAL", 1) != 0 && rbucket <= 4;
+        fin_smax = 0;
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
         for (size_t i = 0; i < mats.size(); ++i) {
@@ -233,8 +289,21 @@ struct psgd_plan {
                 d.odd_sw = d.odd_chunk_rows = 0;
                 d.odd_nstrip = g.nstrip;
             }
+            const FinGeom fg = fin_geometry(d.n, d.m, rbucket, fin_elems);
+            d.fin_T = fg.T;
+            d.fin_S = fg.S;
+            d.fin_rows = fg.rows;
+            fin_smax = std::max(fin_smax, fg.S);
+            // buffer descriptors address one matrix: keep it below 2^31 bytes
+            fin_ok = fin_ok && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
+            for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
         }
+        const int nres_last = iters - 1;
+        fin_ok = fin_ok && fin_bucket(fin_smax) > 0 &&
+                 fin_regs(rbucket, fin_bucket(fin_smax), nres_last) <= 200;
     }
+    // the last iteration of `step` runs fused (odd, and every matrix fits)
+    bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
 
     int upload_tiles() const;
 };
@@ -288,6 +357,7 @@ int psgd_plan::upload_tiles() const {
     if (int st = upload(dev<void>(o_mats), mats.data(), mats.size() * sizeof(MatDesc))) return st;
     if (int st = upload(dev<void>(o_tiles), tiles.data(), tiles.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
+    if (int st = upload(dev<void>(o_tiles_fin), tiles_fin.data(), tiles_fin.size() * sizeof(Tile))) return st;
     return upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile));
 }
 
@@ -394,6 +464,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         return fail(PSGD_ERR_VALUE, "effective rank above 32 is not supported by this build");
     }
     p->rbucket = int(pow2ceil(maxr));
+    p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", 32768));
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
     // whose segment is not 16-byte aligned takes the scalar path
@@ -453,6 +524,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
+        p->tiles_fin_cap += fin_geometry(md.n, md.m, p->rbucket, p->fin_elems).ntiles;
         if (i == 0 || p->mats[i - 1].group != md.group) {
             p->grng_even.push_back(int32_t(p->red_even.size()));
             p->grng_even.push_back(0);
@@ -477,6 +549,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_tiles = carve(size_t(p->tiles_cap) * sizeof(Tile));
     p->o_tiles_ov = carve(size_t(p->tiles_cap) * sizeof(Tile));
     p->o_tiles_om = carve(size_t(std::max<int64_t>(p->tiles_om_cap, 1)) * sizeof(Tile));
+    p->o_tiles_fin = carve(size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(Tile));
     p->o_red_even = carve(p->red_even.size() * sizeof(RedItem));
     p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
@@ -582,13 +655,30 @@ static bool fused_norm(const psgd_plan* p, bool fuse, int it) {
     return fuse && p->rbucket == 1 && it >= 1;
 }
 
+// Timing (benchmarks): HIP events around the final pass (k_apply, or the fused final odd
+// kernel), recorded on the launch stream.
+static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEvent_t>** ev) {
+    *ev = nullptr;
+    if (!p->timing) return PSGD_OK;
+    if (p->ev_used == p->ev_pool.size()) {
+        std::pair<hipEvent_t, hipEvent_t> e;
+        PSGD_HIP(hipEventCreate(&e.first));
+        PSGD_HIP(hipEventCreate(&e.second));
+        p->ev_pool.push_back(e);
+    }
+    *ev = &p->ev_pool[p->ev_used++];
+    PSGD_HIP(hipEventRecord((*ev)->first, s));
+    return PSGD_OK;
+}
+
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
-                         bool fuse) {
+                         bool fuse, bool write_out) {
     if (int st = refresh_pointers(p, grads, s)) return st;
     const bool even = p->even(step, it);
     float* in = even ? p->P : p->Q;
     float* out = even ? p->Q : p->P;
     const bool fused = fused_norm(p, fuse, it);
+    float* ss = p->dev<float>(p->o_ss);
 
     if (!fused) {
         OrthArgs oa{};
@@ -598,6 +688,33 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
         const int nunits = int(even ? p->units_p.size() : p->units_q.size());
         PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+    }
+
+    if (it == p->iters - 1 && p->fused_final(step)) {
+        // last iteration, odd: product + residual (+ output at world size 1) in one pass
+        FinalArgs fa{};
+        fa.mats = p->dev<MatDesc>(p->o_mats);
+        fa.tiles = p->dev<Tile>(p->o_tiles_fin);
+        fa.grads = p->dev<void* const>(p->o_ptrs);
+        fa.out = p->out_now;
+        fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
+        fill_terms(p, step, it, fa.res);
+        fa.nres = it;
+        fa.write_out = write_out ? 1 : 0;
+        fa.yloc = p->hist(1, it);
+        fa.state = out;
+        if (fused) {
+            fa.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
+            fa.grng_in = p->dev<int32_t>(p->o_grng_even);  // in-factor Q came from an even reduce
+            fa.xstate = in;
+            fa.hx = p->hist(0, it);
+        }
+        std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+        if (int st = timing_begin(p, s, &ev)) return st;
+        PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa,
+                                  int(p->tiles_fin.size()), s));
+        if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
+        return PSGD_OK;
     }
 
     ProductArgs pa{};
@@ -629,7 +746,6 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     ra.state = out;
     ra.even = even ? 1 : 0;
     ra.nmain = int(even ? p->red_even.size() : p->red_odd.size());
-    float* ss = p->dev<float>(p->o_ss);
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
         ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
         ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
@@ -649,7 +765,7 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
     DevScope scope(p->device);
-    return compress_impl(p, grads, step, it, static_cast<hipStream_t>(stream), false);
+    return compress_impl(p, grads, step, it, static_cast<hipStream_t>(stream), false, false);
 }
 
 static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
@@ -673,17 +789,13 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     }
     aa.nterms = I;
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
-    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-    if (p->timing) {
-        if (p->ev_used == p->ev_pool.size()) {
-            std::pair<hipEvent_t, hipEvent_t> e;
-            PSGD_HIP(hipEventCreate(&e.first));
-            PSGD_HIP(hipEventCreate(&e.second));
-            p->ev_pool.push_back(e);
-        }
-        ev = &p->ev_pool[p->ev_used++];
-        PSGD_HIP(hipEventRecord(ev->first, s));
+    if (p->fused_final(step)) {
+        // the residual was written by the fused last iteration: output only
+        PSGD_HIP(launch_lowrank_out(p->dtype, p->rbucket, I, aa, int(p->tiles.size()), s));
+        return PSGD_OK;
     }
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (int st = timing_begin(p, s, &ev)) return st;
     PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
     if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
     return PSGD_OK;
@@ -697,6 +809,13 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     DevScope scope(p->device);
     return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false);
+}
+
+int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t* fused) {
+    if (!p || !fused) return fail(PSGD_ERR_VALUE, "null argument");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    *fused = p->fused_final(step) ? 1 : 0;
+    return PSGD_OK;
 }
 
 int psgd_plan_set_timing(psgd_plan* p, int32_t enable) {
@@ -730,8 +849,10 @@ int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, vo
     DevScope scope(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;
+    p->out_now = out;
     for (int it = 0; it < p->iters; ++it)
-        if (int st = compress_impl(p, grads, step, it, s, fuse)) return st;
+        if (int st = compress_impl(p, grads, step, it, s, fuse, true)) return st;
+    if (p->fused_final(step)) return PSGD_OK;  // output written by the fused last iteration
     return decompress_impl(p, grads, out, step, 1, s, fuse);
 }
 

@@ -27,20 +27,6 @@ __device__ unsigned long long g_stamps[64];
     } while (0)
 #endif
 
-// ---------------------------------------------------------------- wave reductions
-// All-reduce of one float over the 64 lanes: 4 DPP row rotations (within rows of 16 lanes),
-// then the gfx950 half-exchanges v_permlane16_swap / v_permlane32_swap. No LDS traffic.
-__device__ __forceinline__ float wave_allsum(float v) {
-    v += dpp<0x128>(v);  // row_ror:8
-    v += dpp<0x124>(v);  // row_ror:4
-    v += dpp<0x122>(v);  // row_ror:2
-    v += dpp<0x121>(v);  // row_ror:1
-    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
-
 // Sum NV floats over a workgroup of NW waves; result in every thread. `red` holds
 // 2 * NW * NV floats (double-buffered by `phase`, so one barrier per call suffices).
 template <int NV, int NW>
@@ -875,18 +861,6 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipSt
 // Sums the partials of each factor element in a FIXED order (row chunks for even
 // iterations, column strips for odd ones): bitwise reproducible, no atomics.
 
-// Joint norm of a rank-1 group from per-item sums of squares (reference
-// orthogonalization.py:5-6: max(||x||, eps)); every workgroup evaluates the same fixed
-// order (lane-strided partial sums, then the DPP/permlane wave tree), so all agree bitwise.
-__device__ __forceinline__ float fused_group_norm(const ReduceArgs& a, int group) {
-    const int lane = threadIdx.x & 63;
-    const int b = a.grng_in[2 * group], e = a.grng_in[2 * group + 1];
-    float ss = 0.f;
-    for (int i = b + lane; i < e; i += 64) ss += a.ss_in[i];
-    const float nrm = sqrtf(wave_allsum(ss));
-    return nrm > 1e-16f ? nrm : 1e-16f;
-}
-
 // One item = kRedElems (64) consecutive elements of one factor; wave w adds the partials
 // [w*np/4, (w+1)*np/4) of each element in order, then wave 0 adds the four wave sums in
 // order: every element is summed in the same fixed order on every run.
@@ -897,7 +871,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         if (wave != 0) return;
         const RedItem it = a.nitems[blockIdx.x - a.nmain];
         const MatDesc d = a.mats[it.mat];
-        const float dn = fused_group_norm(a, d.group);
+        const float dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
         const int64_t len = (a.even ? d.n : d.m) * d.r;
         const int64_t e = int64_t(it.start) + lane;
         if (e < len) {
@@ -931,7 +905,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     __syncthreads();
     if (wave != 0) return;
     s = ((red[lane] + red[kRedElems + lane]) + red[2 * kRedElems + lane]) + red[3 * kRedElems + lane];
-    if (a.ss_in) s = s / fused_group_norm(a, d.group);  // G^T (x / d) == (G^T x) / d up to rounding
+    if (a.ss_in) s = s / group_norm_ss(a.ss_in, a.grng_in, d.group);  // G^T (x / d) == (G^T x) / d up to rounding
     if (e < len) {
         const int64_t dst = (a.even ? d.qoff : d.poff) + e;
         a.yloc[dst] = s;

@@ -183,6 +183,32 @@ __device__ __forceinline__ float sum_across(float v, int L) {
     return v;
 }
 
+// All-reduce of one float over the 64 lanes: 4 DPP row rotations (within rows of 16 lanes),
+// then the gfx950 half-exchanges v_permlane16_swap / v_permlane32_swap. No LDS traffic.
+__device__ __forceinline__ float wave_allsum(float v) {
+    v += dpp<0x128>(v);  // row_ror:8
+    v += dpp<0x124>(v);  // row_ror:4
+    v += dpp<0x122>(v);  // row_ror:2
+    v += dpp<0x121>(v);  // row_ror:1
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// Joint norm of a rank-1 group from per-item sums of squares (reference
+// orthogonalization.py:5-6: max(||x||, eps)); every wave that evaluates it uses the same
+// fixed order (lane-strided partial sums, then the DPP/permlane wave tree), so all agree
+// bitwise. Group g's items are grng[2g] .. grng[2g+1].
+__device__ __forceinline__ float group_norm_ss(const float* ss, const int32_t* grng, int group) {
+    const int lane = threadIdx.x & 63;
+    const int b = grng[2 * group], e = grng[2 * group + 1];
+    float acc = 0.f;
+    for (int i = b + lane; i < e; i += 64) acc += ss[i];
+    const float nrm = sqrtf(wave_allsum(acc));
+    return nrm > 1e-16f ? nrm : 1e-16f;
+}
+
 struct TileGeom {
     int lane, wave, L, sub, ql;
     int64_t n, m, row_begin, row_end, first_row;

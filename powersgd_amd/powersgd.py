@@ -21,6 +21,7 @@ Differences, all deliberate:
 """
 from __future__ import annotations
 
+import ctypes
 import sys
 from abc import ABC, abstractmethod
 from collections import defaultdict
@@ -30,6 +31,14 @@ import torch
 
 from . import _lib
 from .utils import is_distributed
+
+try:
+    from . import _psgd_host  # native gradient split + pointer tables (csrc/psgd_host.cpp)
+except ImportError as e:  # built together with libpsgd.so; no Python fallback
+    raise _lib.LibraryMissing(
+        "powersgd_amd/_psgd_host*.so not found: build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'`"
+    ) from e
 
 _DTYPES = {torch.float32: _lib.PSGD_F32, torch.bfloat16: _lib.PSGD_BF16}
 
@@ -74,11 +83,11 @@ class _OutputSlab:
     def _refs(self) -> List[int]:
         return [sys.getrefcount(v) for v in self.views]
 
-    def get(self, numel: int, like: Sequence[torch.Tensor], dtype, device) -> List[torch.Tensor]:
+    def get(self, numel: int, shapes: Sequence[torch.Size], dtype, device) -> List[torch.Tensor]:
         if self.flat is not None and self._uses() == self._base_uses and self._refs() == self._base_refs:
             return list(self.views)
         flat = torch.empty(max(numel, 1), dtype=dtype, device=device)
-        self.views = list(torch._utils._unflatten_dense_tensors(flat[:numel], list(like)))
+        self.views = _views(flat, shapes)
         self.flat = flat
         self._base_uses = self._uses()
         self._base_refs = self._refs()
@@ -102,38 +111,43 @@ class AllReduce(Aggregator):
     """
 
     def __init__(self):
-        self._plans: Dict[tuple, tuple] = {}
-        self._slab = _OutputSlab()
+        self._plans: Dict[tuple, "_FlatEntry"] = {}
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         if len(gradients) == 0:
             return []
         g0 = gradients[0]
         dev_index = _require_device(g0.device)
-        dtype = g0.dtype
-        code = _dtype_code(dtype)
-        for g in gradients:
-            if g.dtype != dtype or g.device != g0.device:
-                raise RuntimeError("AllReduce expects tensors of one dtype on one device")
-            if not g.is_contiguous():
-                raise RuntimeError("view size is not compatible with input tensor's size and stride")
-        numels = tuple(g.numel() for g in gradients)
-        key = (numels, dtype, g0.device)
+        code = _dtype_code(g0.dtype)
+        key = (tuple(g.shape for g in gradients), g0.dtype, dev_index)
         entry = self._plans.get(key)
         if entry is None:
-            plan = _lib.FlatPlan(numels, code)
-            ws = torch.empty(plan.workspace_bytes(), dtype=torch.uint8, device=g0.device)
-            plan.bind(dev_index, ws.data_ptr())
-            entry = (plan, ws, _OutputSlab())
-            self._plans[key] = entry
-        plan, _, slab = entry
-        total = sum(numels)
-        outs = slab.get(total, gradients, dtype, g0.device)
+            entry = self._plans[key] = _FlatEntry([g.shape for g in gradients], code, g0.dtype, g0.device)
+        _psgd_host.fill_list(gradients, entry.ptr_addr, code, dev_index)
+        return entry.run(entry.ptr_addr)
+
+
+class _FlatEntry:
+    """Flat-pack plan + workspace + pointer table + output slab of one tensor list."""
+
+    def __init__(self, shapes, code: int, dtype, device):
+        self.shapes = [torch.Size(s) for s in shapes]
+        self.numel = sum(s.numel() for s in self.shapes)
+        self.dtype, self.device = dtype, device
+        self.plan = _lib.FlatPlan([s.numel() for s in self.shapes], code)
+        self.ws = torch.empty(self.plan.workspace_bytes(), dtype=torch.uint8, device=device)
+        self.plan.bind(device.index if device.index is not None else torch.cuda.current_device(),
+                       self.ws.data_ptr())
+        self.ptrs = _lib.ptr_array([0] * len(self.shapes))
+        self.ptr_addr = ctypes.addressof(self.ptrs)
+        self.slab = _OutputSlab()
+
+    def run(self, ptr_addr: int) -> List[torch.Tensor]:
+        outs = self.slab.get(self.numel, self.shapes, self.dtype, self.device)
         world = torch.distributed.get_world_size() if is_distributed() else 1
-        ptrs = _lib.ptr_array([g.data_ptr() for g in gradients])
-        plan.pack(ptrs, slab.flat.data_ptr(), world, _stream(g0.device))
+        self.plan.pack(ptr_addr, self.slab.flat.data_ptr(), world, _stream(self.device))
         if is_distributed():
-            torch.distributed.all_reduce(slab.flat[:total])
+            torch.distributed.all_reduce(self.slab.flat[:self.numel])
         return outs
 
 
@@ -161,16 +175,31 @@ class PowerSGD(Aggregator):
             config=BasicConfig(rank=config.rank, num_iters_per_step=config.num_iters_per_step),
         )
         self._allreduce = AllReduce()
+        # native split: one C++ pass checks every gradient and fills the compressed and
+        # uncompressed pointer tables (reference _split :76-84 without Python lists)
+        p = self._powersgd
+        self._table = _psgd_host.PtrTable([list(t.shape) for t in params], self.is_compressed_mask,
+                                          p._code, p._dev_index)
+        unc_shapes = [t.shape for t, c in zip(params, self.is_compressed_mask) if not c]
+        self._unc = _FlatEntry(unc_shapes, p._code, p.dtype, p.device) if unc_shapes else None
+        # _merge order: position of tensor i in (compressed outputs + uncompressed outputs)
+        nc = sum(self.is_compressed_mask)
+        ic, iu, self._order = 0, nc, []
+        for c in self.is_compressed_mask:
+            self._order.append(ic if c else iu)
+            ic, iu = (ic + 1, iu) if c else (ic, iu + 1)
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         self.step_counter += 1
         if self.step_counter <= self.config.start_compressing_after_num_steps:
             return self._allreduce.aggregate(gradients)
-        compressed, uncompressed = self._split(gradients)
-        return self._merge(
-            self._powersgd.aggregate(compressed),
-            self._allreduce.aggregate(uncompressed),
-        )
+        if not isinstance(gradients, list):
+            gradients = list(gradients)
+        self._table.fill(gradients)  # reference _split :76-84 + the checks its torch ops make
+        outs = self._powersgd._aggregate_table(self._table.comp_addr())
+        if self._unc is not None:
+            outs = outs + self._unc.run(self._table.unc_addr())
+        return [outs[i] for i in self._order]  # reference _merge :86-99
 
     def _split(self, params: List[torch.Tensor]):
         comp, unc = [], []
@@ -229,32 +258,21 @@ class BasicPowerSGD(Aggregator):
         self._plan.bind(self._dev_index, self._ps_buffer.data_ptr(), self._qs_buffer.data_ptr(),
                         self._workspace.data_ptr())
         self._out_numel = self._plan.output_numel()
+        self._shapes = [p.shape for p in self.params]
         self._slab = _OutputSlab()
-        self._ptr_key: Optional[tuple] = None
-        self._ptr_arr = None
-
-    def _grad_pointers(self, gradients: List[torch.Tensor]):
-        key = tuple(g.data_ptr() for g in gradients)
-        if key != self._ptr_key:
-            if len(gradients) != len(self.params):
-                raise ValueError(f"expected {len(self.params)} gradients, got {len(gradients)}")
-            for g, p in zip(gradients, self.params):
-                if g.shape != p.shape:
-                    raise RuntimeError(f"gradient shape {tuple(g.shape)} != parameter shape {tuple(p.shape)}")
-                if g.dtype != self.dtype:
-                    raise RuntimeError(f"expected scalar type {self.dtype} but found {g.dtype}")
-                if g.device != self.device:
-                    raise RuntimeError(f"gradient on {g.device}, codec on {self.device}")
-                if not g.is_contiguous():
-                    raise RuntimeError("view size is not compatible with input tensor's size and stride")
-            self._ptr_key = key
-            self._ptr_arr = _lib.ptr_array(key)
-        return self._ptr_arr
+        self._table = _psgd_host.PtrTable([list(s) for s in self._shapes], [True] * len(self._shapes),
+                                          self._code, self._dev_index)
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
-        ptrs = self._grad_pointers(gradients)
-        outs = self._slab.get(self._out_numel, gradients, self.dtype, self.device)
+        if not isinstance(gradients, list):
+            gradients = list(gradients)
+        self._table.fill(gradients)  # dtype / device / shape / contiguity checks + pointers
+        return self._aggregate_table(self._table.comp_addr())
+
+    def _aggregate_table(self, ptrs: int) -> List[torch.Tensor]:
+        """The codec on a native pointer table (address of ``void*[len(params)]``)."""
+        outs = self._slab.get(self._out_numel, self._shapes, self.dtype, self.device)
         out_ptr = self._slab.flat.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter

@@ -28,7 +28,7 @@ print(f"{cfg}: PowerSGD.aggregate wall {wall/K*1e6:.1f} us/step, host inside cal
 
 codec = psgd._powersgd
 comp = [g for g, m in zip(grads, psgd.is_compressed_mask) if m]
-ptrs = codec._grad_pointers(comp)
+codec._table.fill(comp); ptrs = codec._table.comp_addr()
 out = torch.empty(codec._out_numel, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 torch.cuda.synchronize()
