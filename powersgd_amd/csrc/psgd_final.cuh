@@ -23,10 +23,17 @@
 
 namespace psgd {
 
-// Rows per row group per batch: 4 at rank 1 (more bytes in flight per wave), 2 above.
+// Rows per row group per batch (each batch double-buffered: the next batch's loads are in
+// flight while this one reduces and stores): 2, or 1 at rank 4. Workgroup size: 512
+// threads at rank 4 (a row spread over twice the threads keeps the per-thread factor
+// panels, S * 4 * r floats each, within two waves per SIMD), else 256.
 template <int R>
 struct FinRB {
-    static constexpr int value = R == 1 ? 4 : 2;
+    static constexpr int value = R == 4 ? 1 : 2;
+};
+template <int R>
+struct FinNT {
+    static constexpr int value = R == 4 ? 512 : 256;
 };
 
 // Gradient / output rows go through buffer descriptors spanning exactly one matrix: a
@@ -86,15 +93,16 @@ __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c
 
 template <typename T, int R, int K, int SMAX, bool VEC>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
-                                               float (*red)[kWaves][FinRB<R>::value * R]) {
+                                               float (*red)[FinNT<R>::value / 64][FinRB<R>::value * R]) {
     constexpr int RB = FinRB<R>::value;
+    constexpr int NT = FinNT<R>::value;
     constexpr int KC = K > 0 ? K : 1;
     const int r = d.r;
     const int32_t m = int32_t(d.m);
     const int Tg = d.fin_T, S = d.fin_S;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rg = tid / Tg, tt = tid - rg * Tg;
-    const int RGS = kBlock / Tg;
+    const int RGS = NT / Tg;
     const int64_t row0 = int64_t(t.chunk) * d.fin_rows;
     const int64_t row_end = d.n < row0 + d.fin_rows ? d.n : row0 + d.fin_rows;
     const int nres = K >= 0 ? K : a.nres;
@@ -108,7 +116,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     const bool norm = a.ss_in != nullptr;
     const float dn = norm ? group_norm_ss(a.ss_in, a.grng_in, d.group) : 1.f;
     if (norm && t.chunk == 0) {  // row block 0 publishes this matrix's normalised in-factor
-        for (int64_t e = tid; e < d.m * r; e += kBlock) {
+        for (int64_t e = tid; e < d.m * r; e += NT) {
             const float v = X[e] / dn;
             a.xstate[d.qoff + e] = v;
             a.hx[d.qoff + e] = v;
@@ -153,20 +161,23 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                 }
     }
 
-    const int64_t rows = row_end - row0;
-    const int nb = int((rows + int64_t(RGS) * RB - 1) / (int64_t(RGS) * RB));
-    for (int b = 0; b < nb; ++b) {
+    typedef float Rows[RB][SMAX][4];
+    // batch b: rows ib .. ib + RB of row group rg
+    auto load = [&](Rows& g, int b) {
         const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
-        int64_t ic[RB];
-        float g[RB][SMAX][4];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-            ic[u] = ib + u < row_end ? ib + u : row0;  // factor rows: clamped, in range
             const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
 #pragma unroll
             for (int s = 0; s < SMAX; ++s)
                 if (s < S) fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, g[u][s]);
         }
+    };
+    auto process = [&](Rows& g, int b) {
+        const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
+        int64_t ic[RB];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) ic[u] = ib + u < row_end ? ib + u : row0;  // factor rows: clamped
         float ap[KC][RB][R];
         if constexpr (K > 0) {
 #pragma unroll
@@ -294,12 +305,27 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                 }
             }
         }
+    };
+
+    // software pipeline: the next batch's rows are in flight while this batch reduces,
+    // synchronises and stores (the workgroup barrier no longer idles the memory system)
+    const int64_t rows = row_end - row0;
+    const int nb = int((rows + int64_t(RGS) * RB - 1) / (int64_t(RGS) * RB));
+    Rows ga, gb;
+    if (nb > 0) load(ga, 0);
+    for (int b = 0; b < nb; b += 2) {
+        if (b + 1 < nb) load(gb, b + 1);
+        process(ga, b);
+        if (b + 1 < nb) {
+            if (b + 2 < nb) load(ga, b + 2);
+            process(gb, b + 1);
+        }
     }
 }
 
 template <typename T, int R, int K, int SMAX>
-__global__ __launch_bounds__(kBlock) void k_final_odd(FinalArgs a) {
-    __shared__ float red[2][kWaves][FinRB<R>::value * R];
+__global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
+    __shared__ float red[2][FinNT<R>::value / 64][FinRB<R>::value * R];
     const Tile t = a.tiles[blockIdx.x];
     const MatDesc d = a.mats[t.mat];
     if (d.vec)
@@ -365,9 +391,24 @@ __global__ __launch_bounds__(kBlock) void k_lowrank_out(ApplyArgs a) {
 
 // ------------------------------------------------------------------ dispatch ------
 // SMAX (register segments) is the smallest instantiated bucket >= the plan's max fin_S.
+// ntiles == 0: no launch; `*waves` (if non-null) receives the resident waves per SIMD of
+// the instance that would run (the plan only fuses at >= 2).
 template <typename T, int R, int SMAX>
-hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s) {
-    const dim3 grid(ntiles), block(kBlock);
+hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    constexpr int NT = FinNT<R>::value;
+    const dim3 grid(ntiles), block(NT);
+    const void* fn = nres == 0   ? reinterpret_cast<const void*>(&k_final_odd<T, R, 0, SMAX>)
+                     : nres == 1 ? reinterpret_cast<const void*>(&k_final_odd<T, R, 1, SMAX>)
+                                 : reinterpret_cast<const void*>(&k_final_odd<T, R, -1, SMAX>);
+    if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
+        int blocks = 0;
+        hipFuncAttributes fa{};
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, NT, 0);
+        if (e == hipSuccess) e = hipFuncGetAttributes(&fa, fn);
+        if (e != hipSuccess) return e;
+        *waves = fa.localSizeBytes > 0 ? 0 : blocks * (NT / 64) / 4;
+    }
+    if (ntiles == 0) return hipSuccess;
     switch (nres) {
         case 0: k_final_odd<T, R, 0, SMAX><<<grid, block, 0, s>>>(a); break;
         case 1: k_final_odd<T, R, 1, SMAX><<<grid, block, 0, s>>>(a); break;
@@ -377,19 +418,21 @@ hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_
 }
 
 template <typename T, int R>
-hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s) {
-    if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s);
-    if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s);
-    if (smax <= 12) return dispatch_final_k<T, R, 12>(nres, a, ntiles, s);
+hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s, waves);
+    if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
+    if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
+    if (smax <= 12) return dispatch_final_k<T, R, 12>(nres, a, ntiles, s, waves);
     return hipErrorInvalidValue;
 }
 
 template <typename T>
-hipError_t dispatch_final(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s) {
+hipError_t dispatch_final(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
+                          int* waves) {
     switch (R) {
-        case 1: return dispatch_final_r<T, 1>(nres, smax, a, ntiles, s);
-        case 2: return dispatch_final_r<T, 2>(nres, smax, a, ntiles, s);
-        case 4: return dispatch_final_r<T, 4>(nres, smax, a, ntiles, s);
+        case 1: return dispatch_final_r<T, 1>(nres, smax, a, ntiles, s, waves);
+        case 2: return dispatch_final_r<T, 2>(nres, smax, a, ntiles, s, waves);
+        case 4: return dispatch_final_r<T, 4>(nres, smax, a, ntiles, s, waves);
         default: return hipErrorInvalidValue;
     }
 }

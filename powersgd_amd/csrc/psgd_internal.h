@@ -167,8 +167,9 @@ hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int
                            hipStream_t s);
 hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a,
                         int ntiles, hipStream_t s);
+// ntiles == 0: no launch, only the occupancy query (*waves = resident waves per SIMD)
 hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
-                            hipStream_t s);
+                            hipStream_t s, int* waves = nullptr);
 hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, hipStream_t s);

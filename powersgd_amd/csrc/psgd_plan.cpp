@@ -29,15 +29,17 @@ hipError_t launch_apply_bf16(int R, int nterms, bool shared, const ApplyArgs& a,
 hipError_t launch_odd_mfma_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_odd_mfma_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 
-hipError_t launch_final_odd_f32(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s);
-hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_final_odd_f32(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
+                               int* waves);
+hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
+                                int* waves);
 hipError_t launch_lowrank_out_f32(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_lowrank_out_bf16(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 
 hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
-                            hipStream_t s) {
-    return dtype == PSGD_F32 ? launch_final_odd_f32(R, nres, smax, a, ntiles, s)
-                             : launch_final_odd_bf16(R, nres, smax, a, ntiles, s);
+                            hipStream_t s, int* waves) {
+    return dtype == PSGD_F32 ? launch_final_odd_f32(R, nres, smax, a, ntiles, s, waves)
+                             : launch_final_odd_bf16(R, nres, smax, a, ntiles, s, waves);
 }
 hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s) {
     return dtype == PSGD_F32 ? launch_lowrank_out_f32(R, nterms, a, ntiles, s)
@@ -147,13 +149,14 @@ struct FinGeom {
 
 // Fused final odd pass (psgd_final.cuh): row groups of T threads (4 columns each, S
 // segments), fin_rb(R) rows per group per batch, blocks of about fin_elems elements.
-int fin_rb(int R) { return R == 1 ? 4 : 2; }  // == FinRB<R>
+int fin_rb(int R) { return R == 4 ? 1 : 2; }   // == FinRB<R>
+int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
 FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems) {
     FinGeom g;
     const int64_t q4 = (m + 3) / 4;
-    g.T = int(std::min<int64_t>(kBlock, pow2ceil(q4)));
+    g.T = int(std::min<int64_t>(fin_nt(R), pow2ceil(q4)));
     g.S = int((q4 + g.T - 1) / g.T);
-    const int64_t batch = int64_t(kBlock / g.T) * fin_rb(R);  // rows per workgroup batch
+    const int64_t batch = int64_t(fin_nt(R) / g.T) * fin_rb(R);  // rows per workgroup batch
     int64_t rows = round_up(std::max<int64_t>(1, (fin_elems + m - 1) / m), batch);
     // a small matrix must still spread over several workgroups
     rows = std::min(rows, std::max(batch, round_up((n + 7) / 8, batch)));
@@ -163,15 +166,7 @@ FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems) {
     return g;
 }
 
-// VGPR estimate of the fused kernel (cached factor panels + row data + term rows + ~40
-// of addressing and temporaries; calibrated against -Rpass-analysis=kernel-resource-usage,
-// tools/regs.py). Above 200 the kernel drops to one wave per SIMD, so the plan keeps the
-// unfused final iteration instead.
-int fin_regs(int R, int smax, int nres) {
-    const int panels = 1 + (nres == 1 ? 1 : 0);
-    return smax * 4 * R * panels + fin_rb(R) * smax * 4 + 8 * R * fin_rb(R) + 40;
-}
-int fin_bucket(int s) { return s <= 2 ? 2 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
+int fin_bucket(int s) { return s <= 2 ? 2 : s <= 3 ? 3 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
 
 struct DevScope {  // make `dev` current for the scope, restore afterwards
     int prev = -1;
@@ -254,7 +249,11 @@ struct psgd_plan {
         tiles_ov.clear();
         tiles_om.clear();
         tiles_fin.clear();
-        fin_ok = env_int("PSGD_FUSE_FINAL", 1) != 0 && rbucket <= 4;
+        // rank 4 fits (512-thread rows) but measures slower than the unfused kernels
+        // (one row per barrier at m = 4608: too few bytes in flight), so it needs
+        // PSGD_FUSE_FINAL=2 (profiles/r01)
+        const int64_t fuse_mode = env_int("PSGD_FUSE_FINAL", 1);
+        fin_ok = fuse_mode != 0 && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2));
         fin_smax = 0;
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
@@ -298,9 +297,37 @@ struct psgd_plan {
             fin_ok = fin_ok && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
             for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
         }
-        const int nres_last = iters - 1;
-        fin_ok = fin_ok && fin_bucket(fin_smax) > 0 &&
-                 fin_regs(rbucket, fin_bucket(fin_smax), nres_last) <= 200;
+        // fuse only when the instance that would run keeps >= 2 waves per SIMD resident
+        // (its register arrays scale with S * 4 * r; below that the unfused kernels win)
+        fin_ok = fin_ok && fin_bucket(fin_smax) > 0;
+        if (fin_ok) {
+            int waves = 0;
+            FinalArgs none{};
+            fin_ok = launch_final_odd(dtype, rbucket, iters - 1, fin_bucket(fin_smax), none, 0, nullptr,
+                                      &waves) == hipSuccess &&
+                     waves >= 2;
+        }
+        // Optional: largest tiles first (a greedy longest-processing-time order for the
+        // dispatcher, which hands out workgroups in index order as slots free up).
+        // Measured neutral-to-worse on ResNet-50 (profiles/r01), so off by default.
+        if (env_int("PSGD_SORT_TILES", 0)) {
+            auto cost_fin = [&](const Tile& t) {
+                const MatDesc& d = mats[t.mat];
+                return std::min<int64_t>(d.fin_rows, d.n - int64_t(t.chunk) * d.fin_rows) * d.m;
+            };
+            auto cost_col = [&](const Tile& t) {
+                const MatDesc& d = mats[t.mat];
+                const int64_t w = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                return std::min<int64_t>(d.chunk_rows, d.n - int64_t(t.chunk) * d.chunk_rows) *
+                       std::min<int64_t>(w, d.m - int64_t(t.strip) * w);
+            };
+            auto by = [](auto cost) {
+                return [cost](const Tile& a, const Tile& b) { return cost(a) > cost(b); };
+            };
+            std::stable_sort(tiles_fin.begin(), tiles_fin.end(), by(cost_fin));
+            std::stable_sort(tiles.begin(), tiles.end(), by(cost_col));
+            std::stable_sort(tiles_ov.begin(), tiles_ov.end(), by(cost_col));
+        }
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits)
     bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
@@ -464,7 +491,15 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         return fail(PSGD_ERR_VALUE, "effective rank above 32 is not supported by this build");
     }
     p->rbucket = int(pow2ceil(maxr));
-    p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", 32768));
+    {
+        // Fused final pass: ~1500 row blocks on ResNet-50 (about three rounds of the
+        // resident workgroups); the sweeps in profiles/r01 put the optimum at 16-24k
+        // elements per block.
+        int64_t total = 0;
+        for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
+        const int64_t dflt = std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
+        p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
+    }
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
     // whose segment is not 16-byte aligned takes the scalar path
