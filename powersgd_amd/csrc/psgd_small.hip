@@ -79,16 +79,37 @@ __device__ __forceinline__ void block_sum(A (&v)[NV], A* red) {
 //            conventions (beta = -sign(alpha)*||col||, tau = 0 for an all-zero column,
 //            so a zero panel yields the leading identity columns, as torch.linalg.qr does).
 // The panel is staged in LDS when it fits, else worked on in place in the history buffer.
-template <int R>
+// Sum of NV values over a workgroup of NW waves, broadcast to every thread (fixed order).
+template <typename A, int NV, int NW>
+__device__ __forceinline__ void block_sum_nw(A (&v)[NV], A* red) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        for (int s = 32; s > 0; s >>= 1) v[i] += __shfl_xor(v[i], s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[wave * NV + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        A t = red[i];
+        for (int w = 1; w < NW; ++w) t += red[w * NV + i];
+        v[i] = t;
+    }
+}
+
+template <int R, int NT = kBlock>
 __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau) {
     const int tid = threadIdx.x;
     for (int j = 0; j < r; ++j) {
         float s1[1] = {0.f};
-        for (int64_t i = j + 1 + tid; i < k; i += kBlock) {
+        for (int64_t i = j + 1 + tid; i < k; i += NT) {
             const float x = A[i * r + j];
             s1[0] = fmaf(x, x, s1[0]);
         }
-        block_sum<float, 1>(s1, red);
+        block_sum_nw<float, 1, NT / 64>(s1, red);
         const float alpha = A[int64_t(j) * r + j];
         float tj = 0.f;
         if (s1[0] != 0.f) {
@@ -96,7 +117,7 @@ __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau
             const float beta = -copysignf(hypotf(alpha, xnorm), alpha);
             tj = (beta - alpha) / beta;
             const float scal = 1.f / (alpha - beta);
-            for (int64_t i = j + 1 + tid; i < k; i += kBlock) A[i * r + j] *= scal;
+            for (int64_t i = j + 1 + tid; i < k; i += NT) A[i * r + j] *= scal;
             __syncthreads();
             if (tid == 0) A[int64_t(j) * r + j] = beta;
         }
@@ -107,18 +128,18 @@ __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau
             float w[R];
 #pragma unroll
             for (int c = 0; c < R; ++c) w[c] = 0.f;
-            for (int64_t i = j + 1 + tid; i < k; i += kBlock) {
+            for (int64_t i = j + 1 + tid; i < k; i += NT) {
                 const float vi = A[i * r + j];
 #pragma unroll
                 for (int c = 0; c < R; ++c)
                     if (c > j && c < r) w[c] = fmaf(vi, A[i * r + c], w[c]);
             }
-            block_sum<float, R>(w, red);
+            block_sum_nw<float, R, NT / 64>(w, red);
 #pragma unroll
             for (int c = 0; c < R; ++c)
                 if (c > j && c < r) w[c] += A[int64_t(j) * r + c];
             __syncthreads();
-            for (int64_t i = j + tid; i < k; i += kBlock) {
+            for (int64_t i = j + tid; i < k; i += NT) {
                 const float vi = i == j ? 1.f : A[i * r + j];
 #pragma unroll
                 for (int c = 0; c < R; ++c)
@@ -134,18 +155,18 @@ __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau
             float w[R];
 #pragma unroll
             for (int c = 0; c < R; ++c) w[c] = 0.f;
-            for (int64_t i = j + 1 + tid; i < k; i += kBlock) {
+            for (int64_t i = j + 1 + tid; i < k; i += NT) {
                 const float vi = A[i * r + j];
 #pragma unroll
                 for (int c = 0; c < R; ++c)
                     if (c > j && c < r) w[c] = fmaf(vi, A[i * r + c], w[c]);
             }
-            block_sum<float, R>(w, red);
+            block_sum_nw<float, R, NT / 64>(w, red);
 #pragma unroll
             for (int c = 0; c < R; ++c)
                 if (c > j && c < r) w[c] += A[int64_t(j) * r + c];
             __syncthreads();
-            for (int64_t i = j + tid; i < k; i += kBlock) {
+            for (int64_t i = j + tid; i < k; i += NT) {
                 const float vi = i == j ? 1.f : A[i * r + j];
 #pragma unroll
                 for (int c = 0; c < R; ++c)
@@ -153,8 +174,8 @@ __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau
             }
             __syncthreads();
         }
-        for (int64_t i = j + 1 + tid; i < k; i += kBlock) A[i * r + j] *= -tj;
-        for (int64_t i = tid; i < j; i += kBlock) A[i * r + j] = 0.f;
+        for (int64_t i = j + 1 + tid; i < k; i += NT) A[i * r + j] *= -tj;
+        for (int64_t i = tid; i < j; i += NT) A[i * r + j] = 0.f;
         if (tid == 0) A[int64_t(j) * r + j] = 1.f - tj;
         __syncthreads();
     }
@@ -836,11 +857,285 @@ static bool env_orth_wy() {
     return on;
 }
 
+
+// ------------------------------------------- Cholesky QR with LAPACK signs (fast path) ----
+// Q of the Householder QR of a k x r panel X (reference orthogonalization.py:8,
+// torch.linalg.qr) computed as Q = X R^-1 D:
+//   * Gram G = X^T X accumulated in fp64 (one pass over the panel, ONE workgroup
+//     reduction) and its Cholesky factor R (fp64, every thread redundantly);
+//   * D = the column signs LAPACK's geqr2 gives (beta = -sign(alpha) ||x||, and beta =
+//     alpha for a reflector with nothing below the diagonal): read off the top r x r block
+//     of X R^-1 by the LU recursion of Ballard et al., "Reconstructing Householder vectors
+//     from Tall-Skinny QR" (s_j = -sign(pivot_j); last column of a square panel: +sign);
+//   * Q = X (R^-1 D) row by row (fp64, rounded once to fp32).
+// With the Gram in fp64, the loss of orthogonality is ~kappa^2 * 1e-16: below fp32
+// rounding for kappa < 1e4. A panel with a pivot under 1e-8 of its column's squared norm
+// (kappa >~ 1e4, a zero or rank-deficient panel) takes the exact Householder path instead
+// (householder_q above, in place in the history buffer), so zero panels still give the
+// leading identity columns. One workgroup per panel, no register-resident panel: the
+// second pass re-reads it from L2.
+// fp64 all-reduce over the 64 lanes with DPP row rotations + gfx950 half-row swaps on the
+// two 32-bit halves (the fixed order of wave_allsum; no ds_bpermute round trips)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, uint32_t(b), CTRL, 0xf, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, uint32_t(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((uint64_t(hi) << 32) | lo);
+}
+__device__ __forceinline__ double wave_allsum_f64(double v) {
+    v += dpp_f64<0x128>(v);
+    v += dpp_f64<0x124>(v);
+    v += dpp_f64<0x122>(v);
+    v += dpp_f64<0x121>(v);
+    {
+        const uint64_t b = __double_as_longlong(v);
+        const auto l = __builtin_amdgcn_permlane16_swap(uint32_t(b), uint32_t(b), false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(uint32_t(b >> 32), uint32_t(b >> 32), false, false);
+        v = __longlong_as_double((uint64_t(h[0]) << 32) | l[0]) + __longlong_as_double((uint64_t(h[1]) << 32) | l[1]);
+    }
+    {
+        const uint64_t b = __double_as_longlong(v);
+        const auto l = __builtin_amdgcn_permlane32_swap(uint32_t(b), uint32_t(b), false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(uint32_t(b >> 32), uint32_t(b >> 32), false, false);
+        v = __longlong_as_double((uint64_t(h[0]) << 32) | l[0]) + __longlong_as_double((uint64_t(h[1]) << 32) | l[1]);
+    }
+    return v;
+}
+template <int NV, int NW>
+__device__ __forceinline__ void block_sum_f64(double (&v)[NV], double* red) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_allsum_f64(v[i]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[wave * NV + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        double t = red[i];
+        for (int w = 1; w < NW; ++w) t += red[w * NV + i];
+        v[i] = t;
+    }
+}
+
+// NT threads per panel: 512 for r <= 4 (a 4096-row panel is one batch of loads per pass;
+// the kernel is latency-bound, one workgroup per panel), 256 for r = 8 (registers).
+template <int R>
+struct CholNT {
+    static constexpr int value = R <= 4 ? 512 : 256;
+};
+
+// RC = R: the panel has exactly R columns (compile-time rank: the r x r arithmetic is
+// branch-free straight-line fp64 that the compiler interleaves; it is a serial latency
+// chain per workgroup, so this matters); RC = 0: any r <= R at run time.
+template <int R, int RC>
+__device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUnit& u, double* redd, float* red,
+                                                float* tau) {
+    constexpr int NG = R * (R + 1) / 2;
+    constexpr int NT = CholNT<R>::value;
+    const int r = RC > 0 ? RC : u.r;
+    const int64_t k = u.k;
+    const int tid = threadIdx.x;
+    float* __restrict__ st = a.state + u.off;
+    float* __restrict__ hx = a.hx + u.off;
+    float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+
+    // rows in batches of kU per thread, all loads of a batch issued together (clamped
+    // rows, masked afterwards): the panel was just written by another kernel, so each
+    // batch costs one L2/MALL round trip rather than one per row
+    constexpr int kU = R <= 4 ? 8 : 4;
+    double g[NG];
+#pragma unroll
+    for (int e = 0; e < NG; ++e) g[e] = 0.0;
+    for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
+        float x[kU][R];
+#pragma unroll
+        for (int q = 0; q < kU; ++q) {
+            const int64_t i = i0 + int64_t(q) * NT;
+            ld_row<R>(st + (i < k ? i : 0) * r, r, x[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kU; ++q) {
+            const int64_t i = i0 + int64_t(q) * NT;
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                keep(x[q][c]);
+                x[q][c] = i < k ? x[q][c] : 0.f;
+            }
+            if (sv && i < k) st_row<R>(sv + i * r, r, x[q]);
+            int e = 0;
+#pragma unroll
+            for (int c = 0; c < R; ++c)
+#pragma unroll
+                for (int b = c; b < R; ++b) g[e++] += double(x[q][c]) * double(x[q][b]);
+        }
+    }
+    block_sum_f64<NG, NT / 64>(g, redd);
+
+    // Cholesky G = R^T R (upper R, fp64), identical in every thread
+    double Rm[R][R];
+    bool ok = true;
+    {
+        double G[R][R];
+        int e = 0;
+#pragma unroll
+        for (int c = 0; c < R; ++c)
+#pragma unroll
+            for (int b = c; b < R; ++b) {
+                G[c][b] = g[e];
+                G[b][c] = g[e];
+                ++e;
+            }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+#pragma unroll
+            for (int b = 0; b < R; ++b) Rm[j][b] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (j < r) {
+                double piv = G[j][j];
+#pragma unroll
+                for (int l = 0; l < R; ++l)
+                    if (l < j) piv -= Rm[l][j] * Rm[l][j];
+                ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
+                const double d = sqrt(piv > 0.0 ? piv : 1.0);
+                Rm[j][j] = d;
+#pragma unroll
+                for (int b = 0; b < R; ++b)
+                    if (b > j && b < r) {
+                        double v = G[j][b];
+#pragma unroll
+                        for (int l = 0; l < R; ++l)
+                            if (l < j) v -= Rm[l][j] * Rm[l][b];
+                        Rm[j][b] = v / d;
+                    }
+            }
+        }
+    }
+    if (!ok) {  // exact Householder (geqr2 + org2r) in place in the history buffer
+        for (int64_t i = tid; i < k * r; i += NT) hx[i] = st[i];
+        __syncthreads();
+        householder_q<R, NT>(hx, k, r, red, tau);
+        for (int64_t i = tid; i < k * r; i += NT) st[i] = hx[i];
+        return;
+    }
+    // M = R^-1 (upper triangular, back substitution column by column)
+    double M[R][R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+#pragma unroll
+        for (int i = R - 1; i >= 0; --i) {
+            double v = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+            for (int l = 0; l < R; ++l)
+                if (l > i && l < r) v -= Rm[i][l] * M[l][c];
+            M[i][c] = (i < r && c < r) ? v / Rm[i][i] : 0.0;
+        }
+    }
+    // LAPACK column signs from the top block T = X[0:r] M
+    {
+        double T[R][R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            float x[R];
+            ld_row<R>(st + int64_t(i < r ? i : 0) * r, r, x);
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < R; ++l) v += double(x[l]) * M[l][c];
+                T[i][c] = v;
+            }
+        }
+        double sgn[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (j < r) {
+                const bool nonneg = T[j][j] >= 0.0;
+                sgn[j] = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
+                T[j][j] -= sgn[j];
+#pragma unroll
+                for (int i = 0; i < R; ++i)
+                    if (i > j && i < r) {
+                        const double l = T[i][j] / T[j][j];
+#pragma unroll
+                        for (int b = 0; b < R; ++b)
+                            if (b > j && b < r) T[i][b] -= l * T[j][b];
+                    }
+            } else {
+                sgn[j] = 1.0;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int c = 0; c < R; ++c) M[i][c] *= sgn[c];
+    }
+    __syncthreads();  // every thread has read the top block before any row is overwritten
+    for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
+        float x[kU][R];
+#pragma unroll
+        for (int q = 0; q < kU; ++q) {
+            const int64_t i = i0 + int64_t(q) * NT;
+            ld_row<R>(st + (i < k ? i : 0) * r, r, x[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kU; ++q) {
+            const int64_t i = i0 + int64_t(q) * NT;
+#pragma unroll
+            for (int c = 0; c < R; ++c) keep(x[q][c]);
+            float y[R];
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < R; ++l) v += double(x[q][l]) * M[l][c];
+                y[c] = float(v);
+            }
+            if (i < k) {
+                st_row<R>(st + i * r, r, y);
+                st_row<R>(hx + i * r, r, y);
+            }
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
+    constexpr int NT = CholNT<R>::value;
+    __shared__ double redd[NT / 64 * (R * (R + 1) / 2)];
+    __shared__ float red[NT / 64 * R];
+    __shared__ float tau[(R + 3) / 4 * 4];
+    const OrthUnit u = a.units[blockIdx.x];
+    if (u.r == R)
+        orth_chol_panel<R, R>(a, u, redd, red, tau);
+    else
+        orth_chol_panel<R, 0>(a, u, redd, red, tau);
+}
+
+hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s) {
+    switch (R) {
+        case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
+        case 4: k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a); break;
+        case 8: k_orth_chol<8><<<nunits, CholNT<8>::value, 0, s>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
     // register-resident path when the longest rank>1 panel fits RPT * R <= 128 floats/thread
     int64_t rpt = 1;
     while (rpt * kOrthThreads < kmax) rpt <<= 1;
     if (R == 1) return launch_orth_reg_r<1>(1, a, nunits, s);
+    static const bool chol = [] {
+        const char* e = std::getenv("PSGD_ORTH_CHOL");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (chol && R <= 8) return launch_orth_chol(a, nunits, R, s);
     hipError_t err = hipSuccess;
     if (env_orth_wy() && launch_orth_wy(a, nunits, R, kmax, s, &err)) return err;
     if (rpt <= 16 && orth_reg_ok(R, int(rpt))) {
