@@ -22,6 +22,7 @@ Differences, all deliberate:
 from __future__ import annotations
 
 import ctypes
+import os
 import sys
 from abc import ABC, abstractmethod
 from collections import defaultdict
@@ -182,6 +183,8 @@ class PowerSGD(Aggregator):
                                           p._code, p._dev_index)
         unc_shapes = [t.shape for t, c in zip(params, self.is_compressed_mask) if not c]
         self._unc = _FlatEntry(unc_shapes, p._code, p.dtype, p.device) if unc_shapes else None
+        # one fp32 collective can carry factor + uncompressed values (fp32 gradients only)
+        self._merge_ok = p.dtype == torch.float32 and os.environ.get("PSGD_MERGE_ALLREDUCE", "1") != "0"
         # _merge order: position of tensor i in (compressed outputs + uncompressed outputs)
         nc = sum(self.is_compressed_mask)
         ic, iu, self._order = 0, nc, []
@@ -196,10 +199,30 @@ class PowerSGD(Aggregator):
         if not isinstance(gradients, list):
             gradients = list(gradients)
         self._table.fill(gradients)  # reference _split :76-84 + the checks its torch ops make
-        outs = self._powersgd._aggregate_table(self._table.comp_addr())
-        if self._unc is not None:
-            outs = outs + self._unc.run(self._table.unc_addr())
+        if self._unc is not None and is_distributed() and self._merge_ok:
+            outs = self._aggregate_merged()
+        else:
+            outs = self._powersgd._aggregate_table(self._table.comp_addr())
+            if self._unc is not None:
+                outs = outs + self._unc.run(self._table.unc_addr())
         return [outs[i] for i in self._order]  # reference _merge :86-99
+
+    def _aggregate_merged(self) -> List[torch.Tensor]:
+        """World size > 1: ONE collective fewer per step. The uncompressed gradients
+        (divided by W, reference utils.py:43-47) are packed behind the factor the last
+        power iteration produces, and that iteration's SUM all-reduce (:204-209) carries
+        both — on xGMI a sub-MB all-reduce costs its latency, not its bytes."""
+        codec = self._powersgd
+        if codec._p_comm is None:
+            codec._attach_tail(self._unc.numel)
+        comm = codec._last_comm()
+        tail = comm[comm.numel() - self._unc.numel:]
+        world = torch.distributed.get_world_size()
+        self._unc.plan.pack(self._table.unc_addr(), tail.data_ptr(), world, _stream(self.device))
+        outs = codec._aggregate_table(self._table.comp_addr(), last_comm=comm)
+        unc = self._unc.slab.get(self._unc.numel, self._unc.shapes, self._unc.dtype, self.device)
+        self._unc.slab.flat[:self._unc.numel].copy_(tail)
+        return outs + unc
 
     def _split(self, params: List[torch.Tensor]):
         comp, unc = [], []
@@ -262,6 +285,8 @@ class BasicPowerSGD(Aggregator):
         self._slab = _OutputSlab()
         self._table = _psgd_host.PtrTable([list(s) for s in self._shapes], [True] * len(self._shapes),
                                           self._code, self._dev_index)
+        self._p_comm: Optional[torch.Tensor] = None
+        self._q_comm: Optional[torch.Tensor] = None
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
@@ -270,17 +295,42 @@ class BasicPowerSGD(Aggregator):
         self._table.fill(gradients)  # dtype / device / shape / contiguity checks + pointers
         return self._aggregate_table(self._table.comp_addr())
 
-    def _aggregate_table(self, ptrs: int) -> List[torch.Tensor]:
-        """The codec on a native pointer table (address of ``void*[len(params)]``)."""
+    def _attach_tail(self, numel: int) -> None:
+        """Re-home the P and Q state buffers at the head of [factor | tail] allocations so
+        that the last all-reduce of a step can carry ``numel`` more fp32 values (the
+        uncompressed gradients, see PowerSGD._aggregate_merged). State values are kept."""
+        pn, qn = self._ps_buffer.numel(), self._qs_buffer.numel()
+        self._p_comm = torch.zeros(pn + numel, dtype=torch.float32, device=self.device)
+        self._q_comm = torch.zeros(qn + numel, dtype=torch.float32, device=self.device)
+        self._p_comm[:pn].copy_(self._ps_buffer)
+        self._q_comm[:qn].copy_(self._qs_buffer)
+        self._ps_buffer = self._p_comm[:pn]
+        self._qs_buffer = self._q_comm[:qn]
+        self._ps = _views(self._ps_buffer, [p.shape for p in self._ps])
+        self._qs = _views(self._qs_buffer, [q.shape for q in self._qs])
+        self._plan.bind(self._dev_index, self._ps_buffer.data_ptr(), self._qs_buffer.data_ptr(),
+                        self._workspace.data_ptr())
+
+    def _last_comm(self) -> torch.Tensor:
+        """[factor | tail] buffer whose factor the last iteration of this step produces."""
+        last = self.config.num_iters_per_step - 1
+        return self._q_comm if self._plan.out_factor(self.step_counter, last) == 0 else self._p_comm
+
+    def _aggregate_table(self, ptrs: int, last_comm: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+        """The codec on a native pointer table (address of ``void*[len(params)]``).
+        ``last_comm``: all-reduce this [factor | tail] buffer in place of the last factor."""
         outs = self._slab.get(self._out_numel, self._shapes, self.dtype, self.device)
         out_ptr = self._slab.flat.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
         if is_distributed():
             world = torch.distributed.get_world_size()
-            for it in range(self.config.num_iters_per_step):
+            iters = self.config.num_iters_per_step
+            for it in range(iters):
                 self._plan.compress(ptrs, step, it, stream)
                 buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
+                if it == iters - 1 and last_comm is not None:
+                    buf = last_comm
                 torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
             self._plan.decompress(ptrs, out_ptr, step, world, stream)
         else:
