@@ -15,6 +15,7 @@
  *   psgd_aggregate         BasicPowerSGD.aggregate      powersgd/powersgd.py:146-235 (world size 1)
  *   psgd_flat_*            AllReduce.aggregate          powersgd/powersgd.py:22-31,
  *                          pack / allreduce_average      powersgd/utils.py:6-10, :43-49
+ *   psgd_aggregate_flat    PowerSGD.aggregate           powersgd/powersgd.py:64-74 (world size 1)
  *
  * Conventions
  *  - No torch types. Device buffers are plain pointers on the plan's device; `stream` is a
@@ -145,6 +146,14 @@ int psgd_flat_workspace_bytes(const psgd_flat* flat, int64_t* bytes);
 int psgd_flat_bind(psgd_flat* flat, int32_t device, void* workspace);
 int psgd_flat_pack(psgd_flat* flat, void* const* tensors, void* flat_out, int32_t world_size,
                    void* stream);
+
+/* PowerSGD.aggregate at world size 1 in one call (reference powersgd.py:64-74): the codec
+ * step of psgd_aggregate on the compressed tensors `grads`, and the flat pack of the
+ * uncompressed tensors `unc` into `flat_out` (psgd_flat_pack with world size 1) folded into
+ * the codec's final-pass launch as extra workgroups (no launch of its own). Falls back to
+ * two separate calls when the flat plan's dtype or device differs from the codec's. */
+int psgd_aggregate_flat(psgd_plan* plan, void* const* grads, void* out, int64_t step, psgd_flat* flat,
+                        void* const* unc, void* flat_out, void* stream);
 
 #ifdef __cplusplus
 }

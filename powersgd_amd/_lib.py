@@ -44,6 +44,7 @@ _SIGNATURES = {
     "psgd_flat_workspace_bytes": ([_vp, _P_i64], _i32),
     "psgd_flat_bind": ([_vp, _i32, _vp], _i32),
     "psgd_flat_pack": ([_vp, _vp, _vp, _i32, _vp], _i32),
+    "psgd_aggregate_flat": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -169,6 +170,10 @@ class Plan:
 
     def aggregate(self, grads, out_ptr: int, step: int, stream: int) -> None:
         check(lib().psgd_aggregate(self._h, grads, out_ptr, step, stream))
+
+    def aggregate_flat(self, grads, out_ptr: int, step: int, flat: "FlatPlan", unc, flat_out: int,
+                       stream: int) -> None:
+        check(lib().psgd_aggregate_flat(self._h, grads, out_ptr, step, flat._h, unc, flat_out, stream))
 
     def fused_final(self, step: int) -> bool:
         """True when the last iteration of ``step`` runs fused with the final pass."""

@@ -326,7 +326,14 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 template <typename T, int R, int K, int SMAX>
 __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
     __shared__ float red[2][FinNT<R>::value / 64][FinRB<R>::value * R];
-    const Tile t = a.tiles[blockIdx.x];
+    // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
+    // not in the launch tail); then the row blocks
+    const int nf = a.flat.nitems;
+    if (int(blockIdx.x) < nf) {
+        flat_pack_item<T, FinNT<R>::value>(a.flat, blockIdx.x);
+        return;
+    }
+    const Tile t = a.tiles[blockIdx.x - nf];
     const MatDesc d = a.mats[t.mat];
     if (d.vec)
         final_odd_tile<T, R, K, SMAX, true>(a, d, t, red);
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void k_lowrank_out(ApplyArgs a) {
 template <typename T, int R, int SMAX>
 hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     constexpr int NT = FinNT<R>::value;
-    const dim3 grid(ntiles), block(NT);
+    const dim3 grid(ntiles + a.flat.nitems), block(NT);
     const void* fn = nres == 0   ? reinterpret_cast<const void*>(&k_final_odd<T, R, 0, SMAX>)
                      : nres == 1 ? reinterpret_cast<const void*>(&k_final_odd<T, R, 1, SMAX>)
                                  : reinterpret_cast<const void*>(&k_final_odd<T, R, -1, SMAX>);

@@ -66,6 +66,28 @@ struct Terms {
     const float* q[kMaxTerms];
 };
 
+struct FlatEntry {
+    int64_t off, numel;  // dense offset in the flat buffer (non-empty tensors only)
+    int64_t tensor;      // index into the pointer table
+    int64_t pad;
+};
+
+// Flat-pack work item: kFlatItem consecutive elements of one entry.
+constexpr int kFlatItem = 8 * kBlock;
+struct FlatItem {
+    int32_t entry, pad;
+    int64_t start;
+};
+
+struct FlatArgs {
+    const FlatEntry* entries;
+    const FlatItem* items;
+    void* const* tensors;
+    void* flat;
+    int32_t nitems;
+    int32_t world;
+};
+
 struct ProductArgs {
     const MatDesc* mats;
     const Tile* tiles;
@@ -85,6 +107,10 @@ struct ApplyArgs {
     Terms apx;           // all-reduced terms (approximation), scaled by alpha
     int32_t nterms;
     float alpha;         // 1 / world_size
+    // blocks [0, flat.nitems) pack the uncompressed tensors (AllReduce at world size 1)
+    // inside the same launch; the ntiles tiles follow
+    int32_t ntiles;
+    FlatArgs flat;
 };
 
 struct ReduceArgs {
@@ -129,6 +155,8 @@ struct FinalArgs {
     const int32_t* grng_in;
     float* xstate;
     float* hx;
+    int32_t ntiles;       // row blocks; flat pack items come first (as ApplyArgs)
+    FlatArgs flat;
 };
 
 struct OrthArgs {
@@ -136,28 +164,6 @@ struct OrthArgs {
     float* state;        // in-factor state buffer, orthonormalised in place
     float* hx;           // history copy of the orthonormal in-factor
     float* save;         // if non-null: copy of the pre-orthonormalisation values
-};
-
-struct FlatEntry {
-    int64_t off, numel;  // dense offset in the flat buffer (non-empty tensors only)
-    int64_t tensor;      // index into the pointer table
-    int64_t pad;
-};
-
-// Flat-pack work item: kFlatItem consecutive elements of one entry.
-constexpr int kFlatItem = 8 * kBlock;
-struct FlatItem {
-    int32_t entry, pad;
-    int64_t start;
-};
-
-struct FlatArgs {
-    const FlatEntry* entries;
-    const FlatItem* items;
-    void* const* tensors;
-    void* flat;
-    int32_t nitems;
-    int32_t world;
 };
 
 // Host-side launchers (psgd_kernels*.hip). Return hipError_t.

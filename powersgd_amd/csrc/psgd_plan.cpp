@@ -707,7 +707,7 @@ static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEv
 }
 
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
-                         bool fuse, bool write_out) {
+                         bool fuse, bool write_out, const FlatArgs* fl = nullptr) {
     if (int st = refresh_pointers(p, grads, s)) return st;
     const bool even = p->even(step, it);
     float* in = even ? p->P : p->Q;
@@ -744,6 +744,8 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
             fa.xstate = in;
             fa.hx = p->hist(0, it);
         }
+        fa.ntiles = int32_t(p->tiles_fin.size());
+        if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
         if (int st = timing_begin(p, s, &ev)) return st;
         PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa,
@@ -804,7 +806,7 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
 }
 
 static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
-                           hipStream_t s, bool fuse) {
+                           hipStream_t s, bool fuse, const FlatArgs* fl = nullptr) {
     if (int st = refresh_pointers(p, grads, s)) return st;
     const int I = p->iters;
     ApplyArgs aa{};
@@ -826,9 +828,12 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
     if (p->fused_final(step)) {
         // the residual was written by the fused last iteration: output only
+        aa.ntiles = int32_t(p->tiles.size());
         PSGD_HIP(launch_lowrank_out(p->dtype, p->rbucket, I, aa, int(p->tiles.size()), s));
         return PSGD_OK;
     }
+    aa.ntiles = int32_t(p->tiles.size());
+    if (fl) aa.flat = *fl;  // uncompressed tensors ride in the same launch
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (int st = timing_begin(p, s, &ev)) return st;
     PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
@@ -876,19 +881,23 @@ int psgd_plan_timing_read(psgd_plan* p, double* total_ms, int32_t* launches) {
     return PSGD_OK;
 }
 
+static int aggregate_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
+                          const FlatArgs* fl) {
+    static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;
+    p->out_now = out;
+    for (int it = 0; it < p->iters; ++it)
+        if (int st = compress_impl(p, grads, step, it, s, fuse, true, fl)) return st;
+    if (p->fused_final(step)) return PSGD_OK;  // output written by the fused last iteration
+    return decompress_impl(p, grads, out, step, 1, s, fuse, fl);
+}
+
 int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, void* stream) {
     if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     DevScope scope(p->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;
-    p->out_now = out;
-    for (int it = 0; it < p->iters; ++it)
-        if (int st = compress_impl(p, grads, step, it, s, fuse, true)) return st;
-    if (p->fused_final(step)) return PSGD_OK;  // output written by the fused last iteration
-    return decompress_impl(p, grads, out, step, 1, s, fuse);
+    return aggregate_impl(p, grads, out, step, static_cast<hipStream_t>(stream), nullptr);
 }
 
 // ------------------------------------------------------------------ flat pack ------
@@ -942,13 +951,9 @@ int psgd_flat_bind(psgd_flat* f, int32_t device, void* workspace) {
     return PSGD_OK;
 }
 
-int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world, void* stream) {
-    if (!f || (!tensors && f->count > 0) || (!flat && f->total > 0)) return fail(PSGD_ERR_VALUE, "null argument");
-    if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
-    if (world < 1) return fail(PSGD_ERR_VALUE, "world size must be >= 1");
-    if (f->total == 0) return PSGD_OK;
-    DevScope scope(f->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
+// Device-side arguments of a flat pack (uploads the pointer table when it changed).
+static int flat_args(psgd_flat* f, void* const* tensors, void* flat, int32_t world, hipStream_t s,
+                     FlatArgs* out) {
     const size_t n = size_t(f->count);
     bool same = f->host_ptrs.size() == n;
     for (size_t i = 0; same && i < n; ++i) same = f->host_ptrs[i] == tensors[i];
@@ -957,15 +962,46 @@ int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world
         f->host_ptrs.assign(tensors, tensors + n);
         if (int st = upload(f->ws + f->o_ptrs, f->host_ptrs.data(), n * sizeof(void*))) return st;
     }
-    FlatArgs a{};
+    FlatArgs& a = *out;
+    a = FlatArgs{};
     a.entries = reinterpret_cast<const FlatEntry*>(f->ws + f->o_ents);
     a.items = reinterpret_cast<const FlatItem*>(f->ws + f->o_items);
     a.tensors = reinterpret_cast<void* const*>(f->ws + f->o_ptrs);
     a.flat = flat;
     a.nitems = int32_t(f->items.size());
     a.world = world;
+    return PSGD_OK;
+}
+
+int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world, void* stream) {
+    if (!f || (!tensors && f->count > 0) || (!flat && f->total > 0)) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
+    if (world < 1) return fail(PSGD_ERR_VALUE, "world size must be >= 1");
+    if (f->total == 0) return PSGD_OK;
+    DevScope scope(f->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    FlatArgs a;
+    if (int st = flat_args(f, tensors, flat, world, s, &a)) return st;
     PSGD_HIP(launch_flat_pack(f->dtype, a, s));
     return PSGD_OK;
+}
+
+int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f,
+                        void* const* unc, void* flat_out, void* stream) {
+    if (!f || f->total == 0) return psgd_aggregate(p, grads, out, step, stream);
+    if (!p || !grads || !out || !unc || !flat_out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound || !f->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    if (f->dtype != p->dtype || f->device != p->device) {  // separate launches
+        if (int st = psgd_aggregate(p, grads, out, step, stream)) return st;
+        return psgd_flat_pack(f, unc, flat_out, 1, stream);
+    }
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    FlatArgs a;
+    if (int st = flat_args(f, unc, flat_out, 1, s, &a)) return st;
+    return aggregate_impl(p, grads, out, step, s, &a);
 }
 
 }  // extern "C"

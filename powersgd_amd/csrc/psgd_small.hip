@@ -1222,31 +1222,7 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
 // then x = 0. One read + two writes per element.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_flat_pack(FlatArgs a) {
-    const FlatItem it = a.items[blockIdx.x];
-    const FlatEntry en = a.entries[it.entry];
-    const gptr<T> x = gmut<T>(a.tensors[en.tensor]);
-    const gptr<T> f = gmut<T>(a.flat) + en.off;
-    const float w = float(a.world);
-    float v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int64_t j = it.start + int64_t(q) * kBlock + threadIdx.x;
-        float t[1];
-        Io<T>::ld(x + (j < en.numel ? j : 0), t);  // clamped, unconditional
-        v[q] = t[0];
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) keep(v[q]);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int64_t j = it.start + int64_t(q) * kBlock + threadIdx.x;
-        if (j < en.numel) {
-            float t[1] = {a.world != 1 ? v[q] / w : v[q]};
-            Io<T>::st(f + j, t);
-            const float z[1] = {0.f};
-            Io<T>::st(x + j, z);
-        }
-    }
+    flat_pack_item<T, kBlock>(a, blockIdx.x);
 }
 
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s) {

@@ -209,6 +209,39 @@ __device__ __forceinline__ float group_norm_ss(const float* ss, const int32_t* g
     return nrm > 1e-16f ? nrm : 1e-16f;
 }
 
+// One flat-pack item (kFlatItem consecutive elements of one uncompressed tensor; reference
+// powersgd.py:22-31 + utils.py:6-10, :43-49): flat = x / W (division, as div_; an exact
+// copy at W = 1), then x = 0. NT threads; one read + two writes per element.
+template <typename T, int NT>
+__device__ __forceinline__ void flat_pack_item(const FlatArgs& a, int item) {
+    constexpr int PER = kFlatItem / NT;
+    const FlatItem it = a.items[item];
+    const FlatEntry en = a.entries[it.entry];
+    const gptr<T> x = gmut<T>(a.tensors[en.tensor]);
+    const gptr<T> f = gmut<T>(a.flat) + en.off;
+    const float w = float(a.world);
+    float v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int64_t j = it.start + int64_t(q) * NT + threadIdx.x;
+        float t[1];
+        Io<T>::ld(x + (j < en.numel ? j : 0), t);  // clamped, unconditional
+        v[q] = t[0];
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) keep(v[q]);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int64_t j = it.start + int64_t(q) * NT + threadIdx.x;
+        if (j < en.numel) {
+            float t[1] = {a.world != 1 ? v[q] / w : v[q]};
+            Io<T>::st(f + j, t);
+            const float z[1] = {0.f};
+            Io<T>::st(x + j, z);
+        }
+    }
+}
+
 struct TileGeom {
     int lane, wave, L, sub, ql;
     int64_t n, m, row_begin, row_end, first_row;
@@ -909,7 +942,14 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
 
 template <typename T, int R, int NI, bool SHARED>
 __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
-    const Tile t = a.tiles[blockIdx.x];
+    // blocks [0, nitems): uncompressed tensors (first, so they run beside the first wave of
+    // tiles rather than in the launch tail); then the tiles
+    const int nf = a.flat.nitems;
+    if (int(blockIdx.x) < nf) {
+        flat_pack_item<T, kBlock>(a.flat, blockIdx.x);
+        return;
+    }
+    const Tile t = a.tiles[blockIdx.x - nf];
     const MatDesc d = a.mats[t.mat];
     if constexpr (R <= 8) {
         if (d.vec) {
@@ -964,7 +1004,7 @@ hipError_t dispatch_product(int R, bool even, int nres, const ProductArgs& a, in
 
 template <typename T, int R>
 hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s) {
-    const dim3 grid(ntiles), block(kBlock);
+    const dim3 grid(ntiles + a.flat.nitems), block(kBlock);
     constexpr bool kCache = R <= 8;
     const int NI = (kCache && nterms <= 4) ? nterms : -1;
 #define PSGD_A(NN)                                                                       \

@@ -201,6 +201,13 @@ class PowerSGD(Aggregator):
         self._table.fill(gradients)  # reference _split :76-84 + the checks its torch ops make
         if self._unc is not None and is_distributed() and self._merge_ok:
             outs = self._aggregate_merged()
+        elif self._unc is not None and not is_distributed():
+            # world size 1: the uncompressed copy/zero rides in the codec's final launch
+            u = self._unc
+            unc = u.slab.get(u.numel, u.shapes, u.dtype, self.device)
+            outs = self._powersgd._aggregate_table(self._table.comp_addr(),
+                                                   flat=(u.plan, self._table.unc_addr(), u.slab.flat.data_ptr()))
+            outs = outs + unc
         else:
             outs = self._powersgd._aggregate_table(self._table.comp_addr())
             if self._unc is not None:
@@ -316,9 +323,12 @@ class BasicPowerSGD(Aggregator):
         last = self.config.num_iters_per_step - 1
         return self._q_comm if self._plan.out_factor(self.step_counter, last) == 0 else self._p_comm
 
-    def _aggregate_table(self, ptrs: int, last_comm: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+    def _aggregate_table(self, ptrs: int, last_comm: Optional[torch.Tensor] = None,
+                         flat: Optional[tuple] = None) -> List[torch.Tensor]:
         """The codec on a native pointer table (address of ``void*[len(params)]``).
-        ``last_comm``: all-reduce this [factor | tail] buffer in place of the last factor."""
+        ``last_comm``: all-reduce this [factor | tail] buffer in place of the last factor.
+        ``flat``: (FlatPlan, uncompressed pointer table, flat output pointer) packed in the
+        same final launch (world size 1, psgd_aggregate_flat)."""
         outs = self._slab.get(self._out_numel, self._shapes, self.dtype, self.device)
         out_ptr = self._slab.flat.data_ptr()
         stream = _stream(self.device)
@@ -333,6 +343,8 @@ class BasicPowerSGD(Aggregator):
                     buf = last_comm
                 torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
             self._plan.decompress(ptrs, out_ptr, step, world, stream)
+        elif flat is not None:
+            self._plan.aggregate_flat(ptrs, out_ptr, step, flat[0], flat[1], flat[2], stream)
         else:
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
