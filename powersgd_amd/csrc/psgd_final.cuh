@@ -400,14 +400,11 @@ __global__ __launch_bounds__(kBlock) void k_lowrank_out(ApplyArgs a) {
 // SMAX (register segments) is the smallest instantiated bucket >= the plan's max fin_S.
 // ntiles == 0: no launch; `*waves` (if non-null) receives the resident waves per SIMD of
 // the instance that would run (the plan only fuses at >= 2).
-template <typename T, int R, int SMAX>
-hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+template <typename T, int R, int SMAX, int K>
+hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     constexpr int NT = FinNT<R>::value;
-    const dim3 grid(ntiles + a.flat.nitems), block(NT);
-    const void* fn = nres == 0   ? reinterpret_cast<const void*>(&k_final_odd<T, R, 0, SMAX>)
-                     : nres == 1 ? reinterpret_cast<const void*>(&k_final_odd<T, R, 1, SMAX>)
-                                 : reinterpret_cast<const void*>(&k_final_odd<T, R, -1, SMAX>);
     if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
+        const void* fn = reinterpret_cast<const void*>(&k_final_odd<T, R, K, SMAX>);
         int blocks = 0;
         hipFuncAttributes fa{};
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, NT, 0);
@@ -416,20 +413,44 @@ hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_
         *waves = fa.localSizeBytes > 0 ? 0 : blocks * (NT / 64) / 4;
     }
     if (ntiles == 0) return hipSuccess;
-    switch (nres) {
-        case 0: k_final_odd<T, R, 0, SMAX><<<grid, block, 0, s>>>(a); break;
-        case 1: k_final_odd<T, R, 1, SMAX><<<grid, block, 0, s>>>(a); break;
-        default: k_final_odd<T, R, -1, SMAX><<<grid, block, 0, s>>>(a); break;
-    }
+    k_final_odd<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
     return hipGetLastError();
 }
 
+// Earlier terms cached in registers: up to 1 always, up to 3 on narrow rows (SMAX <= 3,
+// e.g. the 4-iteration LSTM config); otherwise read per use from L1/L2 (K = -1).
+// ntiles == 0: no launch; `*waves` (if non-null) receives the resident waves per SIMD of
+// the instance that would run (the plan only fuses at >= 2).
+template <typename T, int R, int SMAX>
+hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    switch (nres) {
+        case 0: return launch_final_k<T, R, SMAX, 0>(a, ntiles, s, waves);
+        case 1: return launch_final_k<T, R, SMAX, 1>(a, ntiles, s, waves);
+        case 2:
+            if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 2>(a, ntiles, s, waves);
+            break;
+        case 3:
+            if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 3>(a, ntiles, s, waves);
+            break;
+        default: break;
+    }
+    return launch_final_k<T, R, SMAX, -1>(a, ntiles, s, waves);
+}
+
+// Instantiated (R, SMAX) pairs: the ones that can keep two waves per SIMD without scratch
+// (tools/regs.py); any other request returns hipErrorInvalidValue and the plan keeps the
+// unfused final iteration.
 template <typename T, int R>
 hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s, waves);
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
-    if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
-    if (smax <= 12) return dispatch_final_k<T, R, 12>(nres, a, ntiles, s, waves);
+    if constexpr (R <= 2) {
+        if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
+        if (smax <= 12 && nres <= 1) {
+            return nres == 0 ? launch_final_k<T, R, 12, 0>(a, ntiles, s, waves)
+                             : launch_final_k<T, R, 12, 1>(a, ntiles, s, waves);
+        }
+    }
     return hipErrorInvalidValue;
 }
 

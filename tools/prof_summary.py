@@ -3,7 +3,8 @@ and per-kernel PMC averages (FETCH_SIZE / WRITE_SIZE, KB per dispatch).
 
 usage: python tools/prof_summary.py <rocprofv3 output dir> [--traffic CFG]
 
---traffic CFG: also merge the per-launch HBM traffic of k_apply (FETCH_SIZE x 2, the gfx950
+--traffic CFG: also merge the per-launch HBM traffic of the final pass (k_final_odd, else
+k_apply; FETCH_SIZE x 2, the gfx950
 16-B streaming-read correction of MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB -> bytes) into
 profiles/pmc_traffic.json under key CFG (read by bench.py for roofline.traffic).
 """
@@ -49,9 +50,13 @@ def main():
         print(f"# {path}")
         for (k, c), v in sorted(acc.items()):
             print(f"{k[:70]:70s} {c:12s} n={len(v):4d} avg={statistics.mean(v):14.1f}")
-            if k.startswith("psgd::k_apply") and c in ("FETCH_SIZE", "WRITE_SIZE"):
-                traffic[c] = statistics.mean(v) * 1024 * (2 if c == "FETCH_SIZE" else 1)
-    if "--traffic" in sys.argv and len(traffic) == 2:
+            # the final pass: k_final_odd (fused last odd iteration) if the run has it, else k_apply
+            if k.startswith(("psgd::k_final_odd", "psgd::k_apply")) and c in ("FETCH_SIZE", "WRITE_SIZE"):
+                prio = 2 if k.startswith("psgd::k_final_odd") else 1
+                if prio >= traffic.get(c + "_prio", 0):
+                    traffic[c] = statistics.mean(v) * 1024 * (2 if c == "FETCH_SIZE" else 1)
+                    traffic[c + "_prio"] = prio
+    if "--traffic" in sys.argv and "FETCH_SIZE" in traffic and "WRITE_SIZE" in traffic:
         cfg = sys.argv[sys.argv.index("--traffic") + 1]
         out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                            "pmc_traffic.json")
