@@ -96,6 +96,10 @@ struct ProductArgs {
     float* part;         // partial-sum workspace
     Terms res;           // error-feedback terms applied on the fly
     int32_t nres;
+    // rank-1 iteration 0 with the norm folded (even product on the RAW state P): strip-0
+    // tiles write sum_rows P^2 of their row chunk to ss0[ss0_base[mat] + chunk]
+    float* ss0;
+    const int32_t* ss0_base;
 };
 
 struct ApplyArgs {

@@ -216,7 +216,12 @@ struct psgd_plan {
     double unc_floats = 0, comp_floats = 0;
     size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_tiles_fin = 0, o_red_even = 0,
            o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, o_grng_even = 0,
-           o_grng_odd = 0, o_ss = 0, ss_stride = 0, ws_bytes = 0;
+           o_grng_odd = 0, o_ss = 0, ss_stride = 0, o_ss0 = 0, o_ss0_base = 0, o_grng_ss0 = 0,
+           ws_bytes = 0;
+    // rank-1 iteration-0 norm fold: per-(matrix, row chunk) sum-of-squares slots of the
+    // even product, and per group the [begin, end) slot range
+    std::vector<int32_t> ss0_base, grng_ss0;
+    int64_t ss0_slots = 0;
     bool bound = false;
     int device = -1;
     float* P = nullptr;
@@ -331,6 +336,7 @@ struct psgd_plan {
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits)
     bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
+    bool fused_final_at(int64_t step, int it) const { return it == iters - 1 && fused_final(step); }
 
     int upload_tiles() const;
 };
@@ -571,6 +577,18 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->grng_even.back() = int32_t(p->red_even.size());
         p->grng_odd.back() = int32_t(p->red_odd.size());
     }
+    for (size_t i = 0; i < p->mats.size(); ++i) {
+        const MatDesc& md = p->mats[i];
+        const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
+        const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
+        if (i == 0 || p->mats[i - 1].group != md.group) {
+            p->grng_ss0.push_back(int32_t(p->ss0_slots));
+            p->grng_ss0.push_back(0);
+        }
+        p->ss0_base.push_back(int32_t(p->ss0_slots));
+        p->ss0_slots += std::max(a.nchunk, b.nchunk);  // unused slots stay zero (bind)
+        p->grng_ss0.back() = int32_t(p->ss0_slots);
+    }
     p->set_vec(p->base_vec);
 
     size_t off = 0;
@@ -593,6 +611,9 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
     p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
     p->o_ss = carve(2 * p->ss_stride * sizeof(float));
+    p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float));
+    p->o_ss0_base = carve(std::max<size_t>(p->ss0_base.size(), 1) * sizeof(int32_t));
+    p->o_grng_ss0 = carve(std::max<size_t>(p->grng_ss0.size(), 1) * sizeof(int32_t));
     p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * sizeof(float));
     p->o_part = carve(size_t(p->part_floats) * sizeof(float));
     p->ws_bytes = off;
@@ -670,6 +691,9 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
+    if (int st = upload(p->dev<void>(p->o_ss0_base), p->ss0_base.data(), p->ss0_base.size() * sizeof(int32_t))) return st;
+    if (int st = upload(p->dev<void>(p->o_grng_ss0), p->grng_ss0.data(), p->grng_ss0.size() * sizeof(int32_t))) return st;
+    PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float)));
     p->bound = true;
     return PSGD_OK;
 }
@@ -688,6 +712,11 @@ int psgd_out_factor(const psgd_plan* p, int64_t step, int32_t it, int32_t* which
 // writes the normalised in-factor (reference powersgd.py:186-188 + orthogonalization.py:5-6).
 static bool fused_norm(const psgd_plan* p, bool fuse, int it) {
     return fuse && p->rbucket == 1 && it >= 1;
+}
+
+static bool norm0_fold() {
+    static const bool on = env_int("PSGD_FUSE_NORM0", 1) != 0;
+    return on;
 }
 
 // Timing (benchmarks): HIP events around the final pass (k_apply, or the fused final odd
@@ -713,9 +742,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     float* in = even ? p->P : p->Q;
     float* out = even ? p->Q : p->P;
     const bool fused = fused_norm(p, fuse, it);
+    // rank 1, iteration 0, even: the joint norm of the (raw) state P is folded into the even
+    // product (per-chunk sums of squares) and its reduction (divide, write normalised P)
+    const bool fused0 = norm0_fold() && p->rbucket == 1 && it == 0 && even && !p->fused_final_at(step, it);
     float* ss = p->dev<float>(p->o_ss);
 
-    if (!fused) {
+    if (!fused && !fused0) {
         OrthArgs oa{};
         oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
         oa.state = in;
@@ -758,8 +790,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     pa.mats = p->dev<MatDesc>(p->o_mats);
     pa.tiles = p->dev<Tile>(p->o_tiles);
     pa.grads = p->dev<void* const>(p->o_ptrs);
-    pa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);  // fused: the raw reduced factor
+    pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
+    if (fused0) {
+        pa.ss0 = p->dev<float>(p->o_ss0);
+        pa.ss0_base = p->dev<int32_t>(p->o_ss0_base);
+    }
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
     if (even) {
@@ -783,6 +819,15 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     ra.state = out;
     ra.even = even ? 1 : 0;
     ra.nmain = int(even ? p->red_even.size() : p->red_odd.size());
+    if (fused0) {  // normalise the state P in place + history copy (P-side items)
+        ra.ss_in = pa.ss0;
+        ra.grng_in = p->dev<int32_t>(p->o_grng_ss0);
+        ra.nitems = p->dev<RedItem>(p->o_red_odd);
+        ra.nnorm = int(p->red_odd.size());
+        ra.raw = in;
+        ra.xstate = in;
+        ra.hx = p->hist(0, it);
+    }
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
         ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
         ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);

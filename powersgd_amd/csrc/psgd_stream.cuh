@@ -536,6 +536,25 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
         }
     }
 
+    if constexpr (EVEN && R == 1) {
+        // iteration-0 norm fold: this chunk's share of the raw in-factor's sum of squares
+        // (written before the partial reduction reuses the LDS scratch)
+        if (a.ss0 && t.strip == 0) {
+            float sq = 0.f;
+            for (int64_t row = g.row_begin + threadIdx.x; row < g.row_end; row += kBlock) {
+                const float x = xp_base[row];
+                sq = fmaf(x, x, sq);
+            }
+            sq = sum_within(sq, 64);
+            if ((threadIdx.x & 63) == 0) lds[g.wave] = sq;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const float tot = ((lds[0] + lds[1]) + lds[2]) + lds[3];
+                a.ss0[a.ss0_base[t.mat] + t.chunk] = tot;
+            }
+            __syncthreads();
+        }
+    }
     if constexpr (EVEN) {
 #pragma unroll
         for (int v = 0; v < V; ++v)
