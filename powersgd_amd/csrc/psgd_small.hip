@@ -974,69 +974,66 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     }
     block_sum_f64<NG, NT / 64>(g, redd);
 
-    // Cholesky G = R^T R (upper R, fp64), identical in every thread
-    double Rm[R][R];
-    bool ok = true;
-    {
-        double G[R][R];
-        int e = 0;
+    // The r x r work (Cholesky, R^-1, LAPACK signs) is a serial fp64 latency chain: wave 0
+    // alone runs it (the other waves would only compete for the fp64 pipes) and publishes
+    // M = R^-1 D through LDS.
+    __shared__ double m_sh[R * R];
+    __shared__ int ok_sh;
+    if ((tid >> 6) == 0) {
+        double Rm[R][R];
+        bool ok = true;
+        {
+            double G[R][R];
+            int e = 0;
 #pragma unroll
-        for (int c = 0; c < R; ++c)
+            for (int c = 0; c < R; ++c)
 #pragma unroll
-            for (int b = c; b < R; ++b) {
-                G[c][b] = g[e];
-                G[b][c] = g[e];
-                ++e;
+                for (int b = c; b < R; ++b) {
+                    G[c][b] = g[e];
+                    G[b][c] = g[e];
+                    ++e;
+                }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+#pragma unroll
+                for (int b = 0; b < R; ++b) Rm[j][b] = 0.0;
             }
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
+            for (int j = 0; j < R; ++j) {
+                if (j < r) {
+                    double piv = G[j][j];
 #pragma unroll
-            for (int b = 0; b < R; ++b) Rm[j][b] = 0.0;
+                    for (int l = 0; l < R; ++l)
+                        if (l < j) piv -= Rm[l][j] * Rm[l][j];
+                    ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
+                    const double d = sqrt(piv > 0.0 ? piv : 1.0);
+                    Rm[j][j] = d;
+#pragma unroll
+                    for (int b = 0; b < R; ++b)
+                        if (b > j && b < r) {
+                            double v = G[j][b];
+#pragma unroll
+                            for (int l = 0; l < R; ++l)
+                                if (l < j) v -= Rm[l][j] * Rm[l][b];
+                            Rm[j][b] = v / d;
+                        }
+                }
+            }
         }
+        // M = R^-1 (upper triangular, back substitution column by column)
+        double M[R][R];
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-            if (j < r) {
-                double piv = G[j][j];
+        for (int c = 0; c < R; ++c) {
+#pragma unroll
+            for (int i = R - 1; i >= 0; --i) {
+                double v = (i == c) ? 1.0 : 0.0;
 #pragma unroll
                 for (int l = 0; l < R; ++l)
-                    if (l < j) piv -= Rm[l][j] * Rm[l][j];
-                ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
-                const double d = sqrt(piv > 0.0 ? piv : 1.0);
-                Rm[j][j] = d;
-#pragma unroll
-                for (int b = 0; b < R; ++b)
-                    if (b > j && b < r) {
-                        double v = G[j][b];
-#pragma unroll
-                        for (int l = 0; l < R; ++l)
-                            if (l < j) v -= Rm[l][j] * Rm[l][b];
-                        Rm[j][b] = v / d;
-                    }
+                    if (l > i && l < r) v -= Rm[i][l] * M[l][c];
+                M[i][c] = (i < r && c < r) ? v / Rm[i][i] : 0.0;
             }
         }
-    }
-    if (!ok) {  // exact Householder (geqr2 + org2r) in place in the history buffer
-        for (int64_t i = tid; i < k * r; i += NT) hx[i] = st[i];
-        __syncthreads();
-        householder_q<R, NT>(hx, k, r, red, tau);
-        for (int64_t i = tid; i < k * r; i += NT) st[i] = hx[i];
-        return;
-    }
-    // M = R^-1 (upper triangular, back substitution column by column)
-    double M[R][R];
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-#pragma unroll
-        for (int i = R - 1; i >= 0; --i) {
-            double v = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-            for (int l = 0; l < R; ++l)
-                if (l > i && l < r) v -= Rm[i][l] * M[l][c];
-            M[i][c] = (i < r && c < r) ? v / Rm[i][i] : 0.0;
-        }
-    }
-    // LAPACK column signs from the top block T = X[0:r] M
-    {
+        // LAPACK column signs from the top block T = X[0:r] M
         double T[R][R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
@@ -1069,11 +1066,27 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
                 sgn[j] = 1.0;
             }
         }
+        if (tid == 0) {
 #pragma unroll
-        for (int i = 0; i < R; ++i)
+            for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int c = 0; c < R; ++c) M[i][c] *= sgn[c];
+                for (int c = 0; c < R; ++c) m_sh[i * R + c] = M[i][c] * sgn[c];
+            ok_sh = ok ? 1 : 0;
+        }
     }
+    __syncthreads();
+    if (!ok_sh) {  // exact Householder (geqr2 + org2r) in place in the history buffer
+        for (int64_t i = tid; i < k * r; i += NT) hx[i] = st[i];
+        __syncthreads();
+        householder_q<R, NT>(hx, k, r, red, tau);
+        for (int64_t i = tid; i < k * r; i += NT) st[i] = hx[i];
+        return;
+    }
+    double M[R][R];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < R; ++c) M[i][c] = m_sh[i * R + c];
     __syncthreads();  // every thread has read the top block before any row is overwritten
     for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
         float x[kU][R];
