@@ -91,12 +91,14 @@ __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c
     }
 }
 
-template <typename T, int R, int K, int SMAX, bool VEC>
+// PL (panels in LDS): the factor panels X and Q_0 of the whole matrix live in LDS (`pan`,
+// [m][R] each, R floats per column) instead of per-thread registers, so a rank-4 row needs no
+// register panels and a 1024-thread workgroup keeps 16 waves of rows in flight.
+template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PL>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
-                                               float (*red)[FinNT<R>::value / 64][FinRB<R>::value * R]) {
-    constexpr int RB = FinRB<R>::value;
-    constexpr int NT = FinNT<R>::value;
+                                               float* red, float* pan) {
     constexpr int KC = K > 0 ? K : 1;
+    constexpr int NW = NT / 64;
     const int r = d.r;
     const int32_t m = int32_t(d.m);
     const int Tg = d.fin_T, S = d.fin_S;
@@ -133,33 +135,105 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     }
     // factor row of column c (clamped to column 0 past the end of a ragged row)
     auto fcol = [&](int s, int v) { return ccol[s] + v < m ? ccol[s] + v : 0; };
-    float xq[SMAX][4][R];
+    float xq[PL ? 1 : SMAX][4][R];
+    float bq[PL ? 1 : KC][PL ? 1 : SMAX][4][R];
+    // LDS panels: component-major [R][mp] (mp = m rounded up to 4, zero padded) so that a
+    // lane's 4 consecutive columns of one component are ONE conflict-free ds_read_b128
+    const int64_t mp = (d.m + 3) & ~int64_t(3);
+    if constexpr (PL) {
+        // one column (R floats, one vector load when r == R) per thread and pass, 8 passes'
+        // loads in flight at once: the fill is a latency chain otherwise
+        constexpr int kFU = 8;
+        for (int64_t j0 = tid; j0 < mp; j0 += int64_t(kFU) * NT) {
+            float xv[kFU][R], bv[kFU][KC][R];
 #pragma unroll
-    for (int s = 0; s < SMAX; ++s) {
-        if (s < S) {
+            for (int q = 0; q < kFU; ++q) {
+                const int64_t j = j0 + int64_t(q) * NT;
+                const int64_t jc = j < d.m ? j : 0;
+                ld_factor<R>(X + jc * r, r, xv[q]);
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                ld_factor<R>(X + fcol(s, v) * r, r, xq[s][v]);
+                for (int k = 0; k < KC; ++k)
+                    if (k < K) ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + jc * r, r, bv[q][k]);
+            }
 #pragma unroll
-                for (int c = 0; c < R; ++c) {
-                    const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
-                    xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
+            for (int q = 0; q < kFU; ++q) {
+                const int64_t j = j0 + int64_t(q) * NT;
+                if (j < mp) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c) {
+                        const float x = j < d.m ? xv[q][c] : 0.f;
+                        pan[c * mp + j] = norm ? x / dn : x;  // matrix.div_ (:6)
+#pragma unroll
+                        for (int k = 0; k < KC; ++k)
+                            if (k < K) pan[(k + 1) * R * mp + c * mp + j] = j < d.m ? bv[q][k][c] : 0.f;
+                    }
                 }
             }
         }
-    }
-    float bq[KC][SMAX][4][R];
-    if constexpr (K > 0) {
+        __syncthreads();
+    } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int s = 0; s < SMAX; ++s) {
+            if (s < S) {
 #pragma unroll
-            for (int s = 0; s < SMAX; ++s)
-                if (s < S) {
+                for (int v = 0; v < 4; ++v) {
+                    ld_factor<R>(X + fcol(s, v) * r, r, xq[s][v]);
 #pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, bq[k][s][v]);
+                    for (int c = 0; c < R; ++c) {
+                        const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
+                        xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
+                    }
                 }
+            }
+        }
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int s = 0; s < SMAX; ++s)
+                    if (s < S) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, bq[k][s][v]);
+                    }
+        }
     }
+    // factor values of the 4 columns of segment s: registers, or R LDS vector reads
+    // (zero past the row end)
+    auto segx = [&](int s, float (&o)[4][R]) {
+        if constexpr (PL) {
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                const v4f q = *reinterpret_cast<const v4f*>(pan + c * mp + ccol[s]);
+                o[0][c] = act[s] ? q.x : 0.f;
+                o[1][c] = act[s] ? q.y : 0.f;
+                o[2][c] = act[s] ? q.z : 0.f;
+                o[3][c] = act[s] ? q.w : 0.f;
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) o[v][c] = xq[s][v][c];
+        }
+    };
+    auto segb = [&](int k, int s, float (&o)[4][R]) {
+        if constexpr (PL) {
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                const v4f q = *reinterpret_cast<const v4f*>(pan + (int64_t(k) + 1) * R * mp + c * mp + ccol[s]);
+                o[0][c] = q.x;
+                o[1][c] = q.y;
+                o[2][c] = q.z;
+                o[3][c] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) o[v][c] = bq[k < KC ? k : 0][s][v][c];
+        }
+    };
 
     typedef float Rows[RB][SMAX][4];
     // batch b: rows ib .. ib + RB of row group rg
@@ -204,9 +278,12 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                     // per-element arithmetic as the product and k_apply
                     if constexpr (K > 0) {
 #pragma unroll
-                        for (int k = 0; k < K; ++k)
+                        for (int k = 0; k < K; ++k) {
+                            float b[4][R];
+                            segb(k, s, b);
 #pragma unroll
-                            for (int v = 0; v < 4; ++v) g[u][s][v] = g[u][s][v] - dotr<R>(ap[k][u], bq[k][s][v]);
+                            for (int v = 0; v < 4; ++v) g[u][s][v] = g[u][s][v] - dotr<R>(ap[k][u], b[v]);
+                        }
                     } else if constexpr (K < 0) {
                         for (int k = 0; k < nres; ++k) {
                             float pa[R];
@@ -219,10 +296,12 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             }
                         }
                     }
+                    float xs[4][R];
+                    segx(s, xs);
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
 #pragma unroll
-                        for (int c = 0; c < R; ++c) dot[u][c] = fmaf(g[u][s][v], xq[s][v][c], dot[u][c]);
+                        for (int c = 0; c < R; ++c) dot[u][c] = fmaf(g[u][s][v], xs[v][c], dot[u][c]);
                 }
             }
         }
@@ -234,7 +313,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
                 for (int c = 0; c < R; ++c) dot[u][c] = sum_within(dot[u][c], Tg);
         } else {
-            float* buf = &red[b & 1][0][0];
+            float* buf = red + (b & 1) * NW * RB * R;
 #pragma unroll
             for (int u = 0; u < RB; ++u)
 #pragma unroll
@@ -279,15 +358,24 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
             for (int s = 0; s < SMAX; ++s) {
                 if (s < S) {
                     float res[4], o[4];
+                    float xs[4][R];
+                    segx(s, xs);
+                    float bs[K > 0 ? K : 1][4][R];
+                    if constexpr (K > 0) {
+                        if (a.write_out) {
+#pragma unroll
+                            for (int k = 0; k < K; ++k) segb(k, s, bs[k]);
+                        }
+                    }
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
-                        const float tl = dotr<R>(pr, xq[s][v]);
+                        const float tl = dotr<R>(pr, xs[v]);
                         res[v] = g[u][s][v] - tl;
                         if (a.write_out) {
                             float acc = 0.f;
                             if constexpr (K > 0) {
 #pragma unroll
-                                for (int k = 0; k < K; ++k) acc = acc + dotr<R>(ap[k][u], bq[k][s][v]);
+                                for (int k = 0; k < K; ++k) acc = acc + dotr<R>(ap[k][u], bs[k][v]);
                             } else if constexpr (K < 0) {
                                 for (int k = 0; k < nres; ++k) {
                                     float pa[R], qb[R];
@@ -325,20 +413,42 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 
 template <typename T, int R, int K, int SMAX>
 __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
-    __shared__ float red[2][FinNT<R>::value / 64][FinRB<R>::value * R];
+    constexpr int NT = FinNT<R>::value, RB = FinRB<R>::value;
+    __shared__ float red[2 * (NT / 64) * RB * R];
     // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
     // not in the launch tail); then the row blocks
     const int nf = a.flat.nitems;
     if (int(blockIdx.x) < nf) {
-        flat_pack_item<T, FinNT<R>::value>(a.flat, blockIdx.x);
+        flat_pack_item<T, NT>(a.flat, blockIdx.x);
         return;
     }
     const Tile t = a.tiles[blockIdx.x - nf];
     const MatDesc d = a.mats[t.mat];
     if (d.vec)
-        final_odd_tile<T, R, K, SMAX, true>(a, d, t, red);
+        final_odd_tile<T, R, K, SMAX, true, NT, RB, false>(a, d, t, red, nullptr);
     else
-        final_odd_tile<T, R, K, SMAX, false>(a, d, t, red);
+        final_odd_tile<T, R, K, SMAX, false, NT, RB, false>(a, d, t, red, nullptr);
+}
+
+// LDS-panel variant: 1024 threads (16 waves), one workgroup per CU (the panels take up to
+// ~150 KB), row groups of up to 512 threads (two rows per barrier at m = 4608).
+constexpr int kFinLdsNT = 1024;
+template <typename T, int R, int K, int SMAX>
+__global__ __launch_bounds__(kFinLdsNT) void k_final_lds(FinalArgs a) {
+    constexpr int NT = kFinLdsNT, RB = 1;
+    __shared__ float red[2 * (NT / 64) * RB * R];
+    extern __shared__ __attribute__((aligned(16))) float pan[];
+    const int nf = a.flat.nitems;
+    if (int(blockIdx.x) < nf) {
+        flat_pack_item<T, NT>(a.flat, blockIdx.x);
+        return;
+    }
+    const Tile t = a.tiles[blockIdx.x - nf];
+    const MatDesc d = a.mats[t.mat];
+    if (d.vec)
+        final_odd_tile<T, R, K, SMAX, true, NT, RB, true>(a, d, t, red, pan);
+    else
+        final_odd_tile<T, R, K, SMAX, false, NT, RB, true>(a, d, t, red, pan);
 }
 
 // output = sum_k alpha * (A_k B_k^T) on the lane-column tiles (same order as k_apply's
@@ -451,6 +561,48 @@ hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, 
                              : launch_final_k<T, R, 12, 1>(a, ntiles, s, waves);
         }
     }
+    return hipErrorInvalidValue;
+}
+
+template <typename T, int R, int SMAX, int K>
+hipError_t launch_final_lds_k(const FinalArgs& a, int ntiles, int lds_bytes, hipStream_t s, int* waves) {
+    const void* fn = reinterpret_cast<const void*>(&k_final_lds<T, R, K, SMAX>);
+    static bool attr = false;  // opt in to > 64 KB of dynamic LDS once per instance
+    if (!attr) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
+        int blocks = 0;
+        hipFuncAttributes fa{};
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kFinLdsNT, size_t(lds_bytes));
+        if (e == hipSuccess) e = hipFuncGetAttributes(&fa, fn);
+        if (e != hipSuccess) return e;
+        *waves = fa.localSizeBytes > 0 ? 0 : blocks * (kFinLdsNT / 64) / 4;
+    }
+    if (ntiles == 0) return hipSuccess;
+    k_final_lds<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(kFinLdsNT), size_t(lds_bytes), s>>>(a);
+    return hipGetLastError();
+}
+
+// LDS-panel instances: ranks 2 and 4, at most one earlier term, rows of <= 3 segments of
+// 4 x 512 columns (row groups of up to 512 threads).
+template <typename T>
+hipError_t dispatch_final_lds(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
+                              hipStream_t s, int* waves) {
+#define PSGD_FL(RR, SS)                                                                               \
+    return nres == 0 ? launch_final_lds_k<T, RR, SS, 0>(a, ntiles, lds_bytes, s, waves)               \
+                     : launch_final_lds_k<T, RR, SS, 1>(a, ntiles, lds_bytes, s, waves)
+    if (nres > 1) return hipErrorInvalidValue;
+    if (R == 2) {
+        if (smax <= 2) PSGD_FL(2, 2);
+        if (smax <= 3) PSGD_FL(2, 3);
+    } else if (R == 4) {
+        if (smax <= 2) PSGD_FL(4, 2);
+        if (smax <= 3) PSGD_FL(4, 3);
+    }
+#undef PSGD_FL
     return hipErrorInvalidValue;
 }
 

@@ -34,6 +34,15 @@ hipError_t launch_final_odd_f32(int R, int nres, int smax, const FinalArgs& a, i
 hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
                                 int* waves);
 hipError_t launch_lowrank_out_f32(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_final_lds_f32(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
+                               hipStream_t s, int* waves);
+hipError_t launch_final_lds_bf16(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
+                                hipStream_t s, int* waves);
+hipError_t launch_final_lds(int dtype, int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
+                            hipStream_t s, int* waves = nullptr) {
+    return dtype == PSGD_F32 ? launch_final_lds_f32(R, nres, smax, lds_bytes, a, ntiles, s, waves)
+                             : launch_final_lds_bf16(R, nres, smax, lds_bytes, a, ntiles, s, waves);
+}
 hipError_t launch_lowrank_out_bf16(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 
 hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
@@ -151,12 +160,17 @@ struct FinGeom {
 // segments), fin_rb(R) rows per group per batch, blocks of about fin_elems elements.
 int fin_rb(int R) { return R == 4 ? 1 : 2; }   // == FinRB<R>
 int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
-FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems) {
+// the two kernel forms: register panels (k_final_odd) and LDS panels (k_final_lds)
+struct FinForm {
+    int nt, tmax, rb;
+};
+FinForm fin_form(int R, bool lds) { return lds ? FinForm{1024, 512, 1} : FinForm{fin_nt(R), fin_nt(R), fin_rb(R)}; }
+FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems) {
     FinGeom g;
     const int64_t q4 = (m + 3) / 4;
-    g.T = int(std::min<int64_t>(fin_nt(R), pow2ceil(q4)));
+    g.T = int(std::min<int64_t>(f.tmax, pow2ceil(q4)));
     g.S = int((q4 + g.T - 1) / g.T);
-    const int64_t batch = int64_t(fin_nt(R) / g.T) * fin_rb(R);  // rows per workgroup batch
+    const int64_t batch = int64_t(f.nt / g.T) * f.rb;  // rows per workgroup batch
     int64_t rows = round_up(std::max<int64_t>(1, (fin_elems + m - 1) / m), batch);
     // a small matrix must still spread over several workgroups
     rows = std::min(rows, std::max(batch, round_up((n + 7) / 8, batch)));
@@ -205,8 +219,10 @@ struct psgd_plan {
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
     std::vector<Tile> tiles_fin; // row blocks of the fused final odd pass
     bool fin_ok = false;         // every matrix fits the fused final odd pass
+    bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
     int fin_smax = 0;
-    int64_t fin_elems = 32768, tiles_fin_cap = 0;
+    int fin_lds_bytes = 0;
+    int64_t fin_elems = 32768, fin_elems_lds = 65536, tiles_fin_cap = 0;
     int64_t tiles_cap = 0, tiles_om_cap = 0;
     std::vector<RedItem> red_even, red_odd;
     std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
@@ -254,12 +270,13 @@ struct psgd_plan {
         tiles_ov.clear();
         tiles_om.clear();
         tiles_fin.clear();
-        // rank 4 fits (512-thread rows) but measures slower than the unfused kernels
-        // (one row per barrier at m = 4608: too few bytes in flight), so it needs
-        // PSGD_FUSE_FINAL=2 (profiles/r01)
+        // PSGD_FUSE_FINAL: 0 off; 1 (default) register panels at ranks 1-2; 2 also allows
+        // the register form at rank 4 (it fits 512-thread rows, but one row per barrier is
+        // too little in flight: slower than unfused); 3 the LDS-panel form at ranks 2-4.
+        // Both rank-4 forms are correct (tests/test_gpu_final.py) but measure slower than
+        // the unfused kernels on ResNet-50 (k_final_lds 96-107 us vs 56 us for k_apply +
+        // 22 us odd product, profiles/r01/sweep_final_lds.txt), so they are opt-in.
         const int64_t fuse_mode = env_int("PSGD_FUSE_FINAL", 1);
-        fin_ok = fuse_mode != 0 && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2));
-        fin_smax = 0;
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
         for (size_t i = 0; i < mats.size(); ++i) {
@@ -293,24 +310,54 @@ struct psgd_plan {
                 d.odd_sw = d.odd_chunk_rows = 0;
                 d.odd_nstrip = g.nstrip;
             }
-            const FinGeom fg = fin_geometry(d.n, d.m, rbucket, fin_elems);
-            d.fin_T = fg.T;
-            d.fin_S = fg.S;
-            d.fin_rows = fg.rows;
-            fin_smax = std::max(fin_smax, fg.S);
-            // buffer descriptors address one matrix: keep it below 2^31 bytes
-            fin_ok = fin_ok && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
-            for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
         }
-        // fuse only when the instance that would run keeps >= 2 waves per SIMD resident
-        // (its register arrays scale with S * 4 * r; below that the unfused kernels win)
-        fin_ok = fin_ok && fin_bucket(fin_smax) > 0;
-        if (fin_ok) {
+        fin_ok = false;
+        fin_lds = false;
+        // buffer descriptors address one matrix: keep each below 2^31 bytes
+        bool small = true;
+        int64_t mmax = 0;
+        for (const MatDesc& d : mats) {
+            small = small && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
+            mmax = std::max(mmax, d.m);
+        }
+        auto try_form = [&](bool lds) {
+            const FinForm f = fin_form(rbucket, lds);
+            int smax = 0;
+            for (const MatDesc& d : mats) smax = std::max(smax, fin_geometry(d.n, d.m, f, 0).S);
             int waves = 0;
             FinalArgs none{};
-            fin_ok = launch_final_odd(dtype, rbucket, iters - 1, fin_bucket(fin_smax), none, 0, nullptr,
-                                      &waves) == hipSuccess &&
-                     waves >= 2;
+            if (lds) {
+                const int64_t bytes = (1 + std::min(iters - 1, 1)) * ((mmax + 3) & ~int64_t(3)) * rbucket *
+                                      int64_t(sizeof(float));
+                if (iters - 1 > 1 || bytes > 150 * 1024) return false;
+                fin_lds_bytes = int(bytes);
+                // one 16-wave workgroup per CU = 4 waves per SIMD
+                return launch_final_lds(dtype, rbucket, iters - 1, smax, fin_lds_bytes, none, 0, nullptr,
+                                        &waves) == hipSuccess && waves >= 4;
+            }
+            // >= 2 waves per SIMD resident (the register arrays scale with S * 4 * r)
+            return fin_bucket(smax) > 0 &&
+                   launch_final_odd(dtype, rbucket, iters - 1, fin_bucket(smax), none, 0, nullptr, &waves) ==
+                       hipSuccess &&
+                   waves >= 2;
+        };
+        if (fuse_mode != 0 && small) {
+            if (fuse_mode != 3 && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2))) fin_ok = try_form(false);
+            if (!fin_ok && fuse_mode == 3 && (rbucket == 2 || rbucket == 4)) fin_ok = fin_lds = try_form(true);
+        }
+        fin_smax = 0;
+        if (fin_ok) {
+            const FinForm f = fin_form(rbucket, fin_lds);
+            const int64_t elems = fin_lds ? fin_elems_lds : fin_elems;
+            for (size_t i = 0; i < mats.size(); ++i) {
+                MatDesc& d = mats[i];
+                const FinGeom fg = fin_geometry(d.n, d.m, f, elems);
+                d.fin_T = fg.T;
+                d.fin_S = fg.S;
+                d.fin_rows = fg.rows;
+                fin_smax = std::max(fin_smax, fg.S);
+                for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
+            }
         }
         // Optional: largest tiles first (a greedy longest-processing-time order for the
         // dispatcher, which hands out workgroups in index order as slots free up).
@@ -505,6 +552,9 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
         const int64_t dflt = std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
+        // LDS form: one workgroup per CU that first loads the matrix's panels, so larger
+        // blocks (~2 rounds over 256 CUs)
+        p->fin_elems_lds = std::max<int64_t>(4096, env_int("PSGD_FIN_ELEMS_LDS", std::max<int64_t>(16384, total / 512)));
     }
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
@@ -565,7 +615,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
-        p->tiles_fin_cap += fin_geometry(md.n, md.m, p->rbucket, p->fin_elems).ntiles;
+        p->tiles_fin_cap += std::max(fin_geometry(md.n, md.m, fin_form(p->rbucket, false), p->fin_elems).ntiles,
+                                     fin_geometry(md.n, md.m, fin_form(p->rbucket, true), p->fin_elems_lds).ntiles);
         if (i == 0 || p->mats[i - 1].group != md.group) {
             p->grng_even.push_back(int32_t(p->red_even.size()));
             p->grng_even.push_back(0);
@@ -780,8 +831,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
         if (int st = timing_begin(p, s, &ev)) return st;
-        PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa,
-                                  int(p->tiles_fin.size()), s));
+        if (p->fin_lds)
+            PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa,
+                                      int(p->tiles_fin.size()), s));
+        else
+            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa,
+                                      int(p->tiles_fin.size()), s));
         if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
         return PSGD_OK;
     }

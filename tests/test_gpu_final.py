@@ -40,7 +40,7 @@ def _rel(a, b, scale):
 
 def _make(shapes, rank, iters, dtype=torch.float32, fuse=True):
     old = os.environ.get("PSGD_FUSE_FINAL")
-    os.environ["PSGD_FUSE_FINAL"] = ("2" if fuse is True else str(int(fuse))) if fuse else "0"
+    os.environ["PSGD_FUSE_FINAL"] = ("2" if fuse is True else str(int(fuse))) if fuse else "0"  # 2, 3 or 0
     try:
         psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dtype) for s in shapes],
                         Config(rank, 0.5, iters, 0))
@@ -57,12 +57,15 @@ def _make(shapes, rank, iters, dtype=torch.float32, fuse=True):
 NARROW = [s for s in SHAPES if int(torch.tensor(s[1:]).prod()) <= 2048]
 
 
-@pytest.mark.parametrize("rank,iters,narrow", [(1, 2, False), (2, 2, False), (1, 1, False), (2, 1, False),
-                                               (1, 3, False), (1, 4, False), (4, 2, False), (2, 3, False),
-                                               (1, 3, True), (2, 4, True), (2, 2, True)])
-def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow):
+# mode: PSGD_FUSE_FINAL for the fused plan (2: register panels allowed at every rank, LDS
+# panels where they do not fit; 3: the LDS-panel kernel k_final_lds forced)
+@pytest.mark.parametrize("rank,iters,narrow,mode", [
+    (1, 2, False, 2), (2, 2, False, 2), (1, 1, False, 2), (2, 1, False, 2), (1, 3, False, 2), (1, 4, False, 2),
+    (4, 2, False, 2), (2, 3, False, 2), (1, 3, True, 2), (2, 4, True, 2), (2, 2, True, 2),
+    (4, 2, False, 3), (2, 2, False, 3), (4, 1, False, 3), (2, 1, True, 3)])
+def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
     shapes = NARROW if narrow else SHAPES
-    fused = _make(shapes, rank, iters, fuse=True)
+    fused = _make(shapes, rank, iters, fuse=mode)
     plain = _make(shapes, rank, iters, fuse=False)
     plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
     plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
@@ -95,7 +98,7 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow):
         plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
         plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
     expect_odd_last = sum(((t * iters + iters - 1) % 2) == 1 for t in range(3))
-    if narrow or (rank == 1 and iters <= 2):  # configurations that must take the fused pass
+    if narrow or (rank == 1 and iters <= 2) or mode == 3:  # configurations that must fuse
         assert n_fused == expect_odd_last, (n_fused, expect_odd_last)
 
 
