@@ -136,6 +136,30 @@ int psgd_plan_fused_final(const psgd_plan* plan, int64_t step, int32_t* fused);
 int psgd_plan_set_timing(psgd_plan* plan, int32_t enable);
 int psgd_plan_timing_read(psgd_plan* plan, double* total_ms, int32_t* launches);
 
+/* ------------------------------- building blocks (paper-code reducer variants) ------ */
+/* The reference repository's paper code (paper-code/gradient_reducers.py) runs PowerSGD as
+ * RankKReducer (:665-788) and HalfRankKReducer (:794-936) with a different call order. These
+ * entry points expose the codec's kernels as steps so that such variants run on the same
+ * plan, layout and kernels (powersgd_amd/reducers.py):
+ *
+ * psgd_product: y = G_k^T x (odd = 0; x P-layout, y Q-layout) or G_k x (odd = 1; x Q-layout,
+ *   y P-layout) for every compressed matrix, G_k = G_0 - sum_{j<nterms} term_p[j] term_q[j]^T
+ *   formed on the fly; no orthonormalisation (torch.matmul(matrix, q) :750 / matrix.t() @ p
+ *   :770). y must not alias x or a term. */
+int psgd_product(psgd_plan* plan, void* const* grads, int32_t odd, const float* x, float* y,
+                 int32_t nterms, const float* const* term_p, const float* const* term_q, void* stream);
+/* In-place orthonormalisation of every panel of a P-layout (which = 1) or Q-layout (0)
+ * buffer. mode 0: the reference codec's (orthogonalization.py:4-8: joint rank-1 norm per
+ * shape group, Householder QR above); mode 1: the paper code's Gram-Schmidt per matrix,
+ * col /= sqrt(sum col^2) + 1e-8 (gradient_reducers.py:945-956). */
+int psgd_orthogonalize(psgd_plan* plan, int32_t which, float* buf, int32_t mode, void* stream);
+/* resid_out[i] <- G_0 - sum_k term_p[k] term_q[k]^T (null resid_out: back into grads[i]) and
+ * out[i] <- alpha * sum_k avg_p[k] avg_q[k]^T, for the compressed tensors i (per-tensor
+ * destination pointers; reference mem.data[:] = tensor - out, out.data[:] = p q^T). */
+int psgd_reconstruct(psgd_plan* plan, void* const* grads, void* const* resid_out, void* const* out,
+                     int32_t nterms, const float* const* term_p, const float* const* term_q,
+                     const float* const* avg_p, const float* const* avg_q, float alpha, void* stream);
+
 /* ------------------------------------------ uncompressed tensors: flat average ------ */
 /* AllReduce.aggregate minus the collective: flat[off_i + e] = x_i[e] / world_size (exact
  * copy when world_size == 1), then x_i[e] = 0. The caller SUM-all-reduces `flat` and

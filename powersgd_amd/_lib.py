@@ -45,6 +45,9 @@ _SIGNATURES = {
     "psgd_flat_bind": ([_vp, _i32, _vp], _i32),
     "psgd_flat_pack": ([_vp, _vp, _vp, _i32, _vp], _i32),
     "psgd_aggregate_flat": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _i32),
+    "psgd_product": ([_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp], _i32),
+    "psgd_orthogonalize": ([_vp, _i32, _vp, _i32, _vp], _i32),
+    "psgd_reconstruct": ([_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, ctypes.c_float, _vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -180,6 +183,22 @@ class Plan:
         f = _i32()
         check(lib().psgd_plan_fused_final(self._h, step, ctypes.byref(f)))
         return bool(f.value)
+
+    # --- building blocks (paper-code reducer variants, powersgd_amd/reducers.py)
+    def product(self, grads, odd: bool, x_ptr: int, y_ptr: int, terms=(), stream: int = 0) -> None:
+        tp = ptr_array([t[0] for t in terms]) if terms else None
+        tq = ptr_array([t[1] for t in terms]) if terms else None
+        check(lib().psgd_product(self._h, grads, 1 if odd else 0, x_ptr, y_ptr, len(terms), tp, tq, stream))
+
+    def orthogonalize(self, which_p: bool, buf_ptr: int, mode: int, stream: int) -> None:
+        check(lib().psgd_orthogonalize(self._h, 1 if which_p else 0, buf_ptr, mode, stream))
+
+    def reconstruct(self, grads, resid_out, out, terms, avg_terms, alpha: float, stream: int) -> None:
+        tp = ptr_array([t[0] for t in terms])
+        tq = ptr_array([t[1] for t in terms])
+        ap = ptr_array([t[0] for t in avg_terms])
+        aq = ptr_array([t[1] for t in avg_terms])
+        check(lib().psgd_reconstruct(self._h, grads, resid_out, out, len(terms), tp, tq, ap, aq, alpha, stream))
 
     def set_timing(self, enable: bool) -> None:
         check(lib().psgd_plan_set_timing(self._h, 1 if enable else 0))

@@ -115,6 +115,11 @@ struct ApplyArgs {
     // inside the same launch; the ntiles tiles follow
     int32_t ntiles;
     FlatArgs flat;
+    // optional destination tables (device arrays of per-tensor pointers): the residual goes
+    // to rdst[i] instead of back into grads[i], the output to odst[i] instead of the flat
+    // buffer (psgd_reconstruct)
+    void* const* rdst;
+    void* const* odst;
 };
 
 struct ReduceArgs {
@@ -183,6 +188,8 @@ hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArg
 hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, hipStream_t s);
+// paper-code Gram-Schmidt (gradient_reducers.py:945-956) on one panel per unit, per matrix
+hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
 
 }  // namespace psgd

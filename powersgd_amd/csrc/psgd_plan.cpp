@@ -227,6 +227,9 @@ struct psgd_plan {
     std::vector<RedItem> red_even, red_odd;
     std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
     std::vector<OrthUnit> units_p, units_q;
+    std::vector<OrthUnit> munits_p, munits_q;  // one unit per MATRIX (paper-code Gram-Schmidt)
+    size_t o_munits_p = 0, o_munits_q = 0, o_rdst = 0, o_odst = 0;
+    std::vector<void*> host_rdst, host_odst;
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_floats = 0;
     double unc_floats = 0, comp_floats = 0;
@@ -658,6 +661,14 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
     p->o_units_q = carve(p->units_q.size() * sizeof(OrthUnit));
+    for (const MatDesc& md : p->mats) {
+        p->munits_p.push_back(OrthUnit{md.poff, md.n, md.r, 1});
+        p->munits_q.push_back(OrthUnit{md.qoff, md.m, md.r, 1});
+    }
+    p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
+    p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
+    p->o_rdst = carve(size_t(num_tensors) * sizeof(void*));
+    p->o_odst = carve(size_t(num_tensors) * sizeof(void*));
     p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
     p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
     p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
@@ -739,6 +750,10 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     if (int st = upload(p->dev<void>(p->o_red_even), p->red_even.data(), p->red_even.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
+    if (int st = upload(p->dev<void>(p->o_munits_p), p->munits_p.data(), p->munits_p.size() * sizeof(OrthUnit))) return st;
+    if (int st = upload(p->dev<void>(p->o_munits_q), p->munits_q.data(), p->munits_q.size() * sizeof(OrthUnit))) return st;
+    p->host_rdst.clear();
+    p->host_odst.clear();
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
@@ -949,6 +964,130 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     DevScope scope(p->device);
     return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false);
+}
+
+// ------------------------------------------------- building blocks (reducer variants) ---
+static int check_terms(int32_t nterms, const float* const* a, const float* const* b) {
+    if (nterms < 0 || nterms > kMaxTerms) return fail(PSGD_ERR_VALUE, "term count out of range");
+    for (int k = 0; k < nterms; ++k)
+        if (!a || !b || !a[k] || !b[k]) return fail(PSGD_ERR_VALUE, "null term buffer");
+    return PSGD_OK;
+}
+
+int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, float* y, int32_t nterms,
+                 const float* const* term_p, const float* const* term_q, void* stream) {
+    if (!p || !grads || !x || !y) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (int st = check_terms(nterms, term_p, term_q)) return st;
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    ProductArgs pa{};
+    pa.mats = p->dev<MatDesc>(p->o_mats);
+    pa.grads = p->dev<void* const>(p->o_ptrs);
+    pa.x = x;
+    pa.part = p->dev<float>(p->o_part);
+    for (int k = 0; k < nterms; ++k) {
+        pa.res.p[k] = term_p[k];
+        pa.res.q[k] = term_q[k];
+    }
+    pa.nres = nterms;
+    if (!odd) {
+        pa.tiles = p->dev<Tile>(p->o_tiles);
+        PSGD_HIP(launch_product(p->dtype, p->rbucket, true, nterms, pa, int(p->tiles.size()), s));
+    } else {
+        if (!p->tiles_ov.empty()) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_ov);
+            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, nterms, pa, int(p->tiles_ov.size()), s));
+        }
+        if (!p->tiles_om.empty()) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_om);
+            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), nterms, pa, int(p->tiles_om.size()), s));
+        }
+    }
+    ReduceArgs ra{};
+    ra.mats = pa.mats;
+    ra.items = p->dev<RedItem>(odd ? p->o_red_odd : p->o_red_even);
+    ra.part = pa.part;
+    ra.yloc = y;
+    ra.state = y;
+    ra.even = odd ? 0 : 1;
+    ra.nmain = int(odd ? p->red_odd.size() : p->red_even.size());
+    PSGD_HIP(launch_reduce(ra, ra.nmain, s));
+    return PSGD_OK;
+}
+
+int psgd_orthogonalize(psgd_plan* p, int32_t which, float* buf, int32_t mode, void* stream) {
+    if (!p || !buf) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (mode != 0 && mode != 1) return fail(PSGD_ERR_VALUE, "mode must be 0 (reference) or 1 (paper-code)");
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    OrthArgs oa{};
+    oa.state = buf;
+    oa.hx = p->hist(0, 0);  // scratch copy
+    if (mode == 1) {
+        oa.units = p->dev<OrthUnit>(which ? p->o_munits_p : p->o_munits_q);
+        PSGD_HIP(launch_orth_mgs(oa, int(p->mats.size()), p->rbucket, s));
+    } else {
+        oa.units = p->dev<OrthUnit>(which ? p->o_units_p : p->o_units_q);
+        const int nunits = int(which ? p->units_p.size() : p->units_q.size());
+        PSGD_HIP(launch_orth(oa, nunits, p->rbucket, which ? p->panel_p : p->panel_q, s));
+    }
+    return PSGD_OK;
+}
+
+// upload a per-tensor destination table when it changed; every pointer must keep the
+// vector layout's alignment where the matrix uses it
+static int refresh_table(psgd_plan* p, void* const* ptrs, std::vector<void*>& host, size_t off, hipStream_t s) {
+    const size_t nt = p->shapes.size();
+    const uintptr_t need = p->dtype == PSGD_F32 ? 16 : 8;
+    for (const MatDesc& md : p->mats) {
+        if (!ptrs[md.tensor]) return fail(PSGD_ERR_VALUE, "null destination pointer");
+        if (md.vec && reinterpret_cast<uintptr_t>(ptrs[md.tensor]) % need)
+            return fail(PSGD_ERR_LAYOUT, "destination tensor is not aligned for the vector layout");
+    }
+    bool same = host.size() == nt;
+    for (size_t i = 0; same && i < nt; ++i) same = host[i] == ptrs[i];
+    if (same) return PSGD_OK;
+    PSGD_HIP(hipStreamSynchronize(s));
+    host.assign(ptrs, ptrs + nt);
+    return upload(p->dev<void>(off), host.data(), nt * sizeof(void*));
+}
+
+int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, void* const* out, int32_t nterms,
+                     const float* const* term_p, const float* const* term_q, const float* const* avg_p,
+                     const float* const* avg_q, float alpha, void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (nterms < 1) return fail(PSGD_ERR_VALUE, "at least one term");
+    if (int st = check_terms(nterms, term_p, term_q)) return st;
+    if (int st = check_terms(nterms, avg_p, avg_q)) return st;
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    if (resid_out)
+        if (int st = refresh_table(p, resid_out, p->host_rdst, p->o_rdst, s)) return st;
+    if (int st = refresh_table(p, out, p->host_odst, p->o_odst, s)) return st;
+    ApplyArgs aa{};
+    aa.mats = p->dev<MatDesc>(p->o_mats);
+    aa.tiles = p->dev<Tile>(p->o_tiles);
+    aa.grads = p->dev<void* const>(p->o_ptrs);
+    aa.rdst = resid_out ? p->dev<void* const>(p->o_rdst) : nullptr;
+    aa.odst = p->dev<void* const>(p->o_odst);
+    bool shared = alpha == 1.0f;
+    for (int k = 0; k < nterms; ++k) {
+        aa.res.p[k] = term_p[k];
+        aa.res.q[k] = term_q[k];
+        aa.apx.p[k] = avg_p[k];
+        aa.apx.q[k] = avg_q[k];
+        shared = shared && avg_p[k] == term_p[k] && avg_q[k] == term_q[k];
+    }
+    aa.nterms = nterms;
+    aa.alpha = alpha;
+    aa.ntiles = int32_t(p->tiles.size());
+    PSGD_HIP(launch_apply(p->dtype, p->rbucket, nterms, shared, aa, int(p->tiles.size()), s));
+    return PSGD_OK;
 }
 
 int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t* fused) {

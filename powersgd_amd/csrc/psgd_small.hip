@@ -1139,6 +1139,64 @@ hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s)
     return hipGetLastError();
 }
 
+// ------------------------------------------------ paper-code Gram-Schmidt (variant) ----
+// paper-code/gradient_reducers.py:945-956 (RankKReducer / HalfRankKReducer), per matrix:
+//   for i: col_i /= sqrt(sum col_i^2) + 1e-8 ; rest -= (col_i . rest) col_i
+// (the eps is ADDED to the norm, unlike the reference codec's max(norm, eps)). One
+// workgroup per panel, in place, column sums as fixed-order workgroup reductions.
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_orth_mgs(OrthArgs a) {
+    __shared__ float red[kWaves * R];
+    const OrthUnit u = a.units[blockIdx.x];
+    const int r = u.r;
+    const int64_t k = u.k;
+    const int tid = threadIdx.x;
+    float* __restrict__ x = a.state + u.off;
+    for (int i = 0; i < r; ++i) {
+        float s1[1] = {0.f};
+        for (int64_t row = tid; row < k; row += kBlock) {
+            const float v = x[row * r + i];
+            s1[0] = fmaf(v, v, s1[0]);
+        }
+        block_sum_nw<float, 1, kWaves>(s1, red);
+        const float den = sqrtf(s1[0]) + 1e-8f;
+        for (int64_t row = tid; row < k; row += kBlock) x[row * r + i] = x[row * r + i] / den;
+        __syncthreads();
+        if (i + 1 < r) {
+            float dt[R];
+#pragma unroll
+            for (int c = 0; c < R; ++c) dt[c] = 0.f;
+            for (int64_t row = tid; row < k; row += kBlock) {
+                const float ci = x[row * r + i];
+#pragma unroll
+                for (int c = 0; c < R; ++c)
+                    if (c > i && c < r) dt[c] = fmaf(ci, x[row * r + c], dt[c]);
+            }
+            block_sum_nw<float, R, kWaves>(dt, red);
+            for (int64_t row = tid; row < k; row += kBlock) {
+                const float ci = x[row * r + i];
+#pragma unroll
+                for (int c = 0; c < R; ++c)
+                    if (c > i && c < r) x[row * r + c] -= dt[c] * ci;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s) {
+    switch (R) {
+        case 1: k_orth_mgs<1><<<nunits, kBlock, 0, s>>>(a); break;
+        case 2: k_orth_mgs<2><<<nunits, kBlock, 0, s>>>(a); break;
+        case 4: k_orth_mgs<4><<<nunits, kBlock, 0, s>>>(a); break;
+        case 8: k_orth_mgs<8><<<nunits, kBlock, 0, s>>>(a); break;
+        case 16: k_orth_mgs<16><<<nunits, kBlock, 0, s>>>(a); break;
+        case 32: k_orth_mgs<32><<<nunits, kBlock, 0, s>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
     // register-resident path when the longest rank>1 panel fits RPT * R <= 128 floats/thread
     int64_t rpt = 1;

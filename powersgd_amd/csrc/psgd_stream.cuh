@@ -887,7 +887,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
     const gptr<T> G = gmut<T>(a.grads[d.tensor]);
-    const gptr<T> O = gmut<T>(a.out) + d.out_off;
+    const gptr<T> D = a.rdst ? gmut<T>(a.rdst[d.tensor]) : G;  // residual destination
+    const gptr<T> O = a.odst ? gmut<T>(a.odst[d.tensor]) : gmut<T>(a.out) + d.out_off;
     const int nt = NI > 0 ? NI : a.nterms;
     constexpr int NC = NI > 0 ? NI : 1;
     constexpr int NA = (NI > 0 && !SHARED) ? NI : 1;
@@ -952,7 +953,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
                 }
             }
             if (g.active && row + u * g.stride < g.row_end) {
-                Io<T>::st(G + rc[u] * g.m + g.col0, x[u]);
+                Io<T>::st(D + rc[u] * g.m + g.col0, x[u]);
                 Io<T>::st(O + rc[u] * g.m + g.col0, o);
             }
         }
