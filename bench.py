@@ -134,8 +134,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0
+        # over gloo exercises the N > 1 code path end to end; the real run is RCCL, one GPU
+        # per rank
+        if os.environ.get("PSGD_BENCH_ONE_DEVICE") == "1":
+            local = 0
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("PSGD_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     dev = torch.device("cuda", local)
     c = dict(CONFIGS[a.config])
     c["name"] = a.config
