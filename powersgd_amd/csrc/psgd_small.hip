@@ -232,7 +232,8 @@ constexpr int kOrthWaves = kOrthThreads / 64;
 
 // rank 1: x /= max(||x||, 1e-16) over the whole shape group (two streaming passes, the
 // second one from L2). Optionally saves the pre-normalisation values.
-__device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red) {
+template <int NT = kOrthThreads>
+__device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, double* rd) {
     float* __restrict__ st = a.state + u.off;
     float* __restrict__ hx = a.hx + u.off;
     float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
@@ -240,16 +241,16 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red
     const int tid = threadIdx.x;
     constexpr int U = 8;
     float part = 0.f;
-    for (int64_t base = tid; base < total; base += int64_t(U) * kOrthThreads) {
+    for (int64_t base = tid; base < total; base += int64_t(U) * NT) {
         float x[U];
 #pragma unroll
         for (int q = 0; q < U; ++q) {  // unconditional loads from clamped indices (no branches)
-            const int64_t i = base + int64_t(q) * kOrthThreads;
+            const int64_t i = base + int64_t(q) * NT;
             x[q] = st[i < total ? i : 0];
         }
 #pragma unroll
         for (int q = 0; q < U; ++q) {
-            const int64_t i = base + int64_t(q) * kOrthThreads;
+            const int64_t i = base + int64_t(q) * NT;
             keep(x[q]);
             x[q] = i < total ? x[q] : 0.f;
         }
@@ -258,26 +259,25 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, float* red
     }
     // block sum in double (wave partials in fp32 are exact enough: <= 64 * U terms each)
     double s = wave_allsum(part);
-    double* rd = reinterpret_cast<double*>(red);
     if ((tid & 63) == 0) rd[tid >> 6] = s;
     __syncthreads();
     s = 0.0;
 #pragma unroll
-    for (int w = 0; w < kOrthWaves; ++w) s += rd[w];
+    for (int w = 0; w < NT / 64; ++w) s += rd[w];
     const float nrm = float(sqrt(s));
     const float d = nrm > 1e-16f ? nrm : 1e-16f;  // torch.maximum(norm, eps)
-    for (int64_t base = tid; base < total; base += int64_t(U) * kOrthThreads) {
+    for (int64_t base = tid; base < total; base += int64_t(U) * NT) {
         float x[U];
 #pragma unroll
         for (int q = 0; q < U; ++q) {
-            const int64_t i = base + int64_t(q) * kOrthThreads;
+            const int64_t i = base + int64_t(q) * NT;
             x[q] = st[i < total ? i : 0];
         }
 #pragma unroll
         for (int q = 0; q < U; ++q) keep(x[q]);
 #pragma unroll
         for (int q = 0; q < U; ++q) {
-            const int64_t i = base + int64_t(q) * kOrthThreads;
+            const int64_t i = base + int64_t(q) * NT;
             if (i < total) {
                 if (sv) sv[i] = x[q];
                 const float y = x[q] / d;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
     __shared__ __attribute__((aligned(16))) float red[2 * kOrthWaves * (R > 2 ? R : 2)];
     const OrthUnit u = a.units[blockIdx.x];
     if (u.r == 1) {
-        orth_joint_norm(a, u, red);
+        orth_joint_norm(a, u, reinterpret_cast<double*>(red));
         return;
     }
     if constexpr (R > 1) {
@@ -1123,7 +1123,9 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
     __shared__ float red[NT / 64 * R];
     __shared__ float tau[(R + 3) / 4 * 4];
     const OrthUnit u = a.units[blockIdx.x];
-    if (u.r == R)
+    if (u.r == 1)  // rank-1 group of a mixed-rank plan: the reference's joint norm, not QR
+        orth_joint_norm<NT>(a, u, redd);
+    else if (u.r == R)
         orth_chol_panel<R, R>(a, u, redd, red, tau);
     else
         orth_chol_panel<R, 0>(a, u, redd, red, tau);
