@@ -10,7 +10,8 @@ import os
 from typing import List, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libpsgd.so")
+# PSGD_LIB_PATH: an alternative in-tree build (tuning variants); default the standard one
+LIB_PATH = os.environ.get("PSGD_LIB_PATH") or os.path.join(_HERE, "_lib", "libpsgd.so")
 
 PSGD_F32, PSGD_BF16 = 0, 1
 _STATUS_NAMES = {1: "INDEX", 2: "VALUE", 3: "DTYPE", 4: "LAYOUT", 5: "DEVICE", 6: "STATE"}

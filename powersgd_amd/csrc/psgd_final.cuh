@@ -27,9 +27,12 @@ namespace psgd {
 // flight while this one reduces and stores): 2, or 1 at rank 4. Workgroup size: 512
 // threads at rank 4 (a row spread over twice the threads keeps the per-thread factor
 // panels, S * 4 * r floats each, within two waves per SIMD), else 256.
+#ifndef PSGD_FIN_RB12
+#define PSGD_FIN_RB12 2
+#endif
 template <int R>
 struct FinRB {
-    static constexpr int value = R == 4 ? 1 : 2;
+    static constexpr int value = R == 4 ? 1 : PSGD_FIN_RB12;
 };
 template <int R>
 struct FinNT {
@@ -172,31 +175,37 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         }
         __syncthreads();
     } else {
+        // every panel load issued unconditionally (clamped columns) before any is consumed:
+        // a load under a lane condition becomes a branch with its own wait, i.e. a chain of
+        // SMAX * 4 * (K + 1) round trips before the first gradient row
 #pragma unroll
-        for (int s = 0; s < SMAX; ++s) {
-            if (s < S) {
+        for (int s = 0; s < SMAX; ++s)
 #pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    ld_factor<R>(X + fcol(s, v) * r, r, xq[s][v]);
-#pragma unroll
-                    for (int c = 0; c < R; ++c) {
-                        const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
-                        xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
-                    }
-                }
-            }
-        }
+            for (int v = 0; v < 4; ++v) ld_factor<R>(X + fcol(s, v) * r, r, xq[s][v]);
         if constexpr (K > 0) {
 #pragma unroll
             for (int k = 0; k < K; ++k)
 #pragma unroll
                 for (int s = 0; s < SMAX; ++s)
-                    if (s < S) {
 #pragma unroll
-                        for (int v = 0; v < 4; ++v)
-                            ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, bq[k][s][v]);
-                    }
+                    for (int v = 0; v < 4; ++v)
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + fcol(s, v) * r, r, bq[k][s][v]);
         }
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) keep(xq[s][v][c]);
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
+                    xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
+                }
     }
     // factor values of the 4 columns of segment s: registers, or R LDS vector reads
     // (zero past the row end)
@@ -235,45 +244,55 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         }
     };
 
-    typedef float Rows[RB][SMAX][4];
-    // batch b: rows ib .. ib + RB of row group rg
-    auto load = [&](Rows& g, int b) {
+    // one batch: rows ib .. ib + RB of row group rg, with their error-feedback factor rows.
+    // Every load of a batch is issued unconditionally (rows past the block end and
+    // segments past the row end load 0 through kOob / clamped factor rows), so the number
+    // of loads in flight is the same on every path and the waits stay counted, not full
+    struct Batch {
+        float g[RB][SMAX][4];
+        float ap[KC][RB][R];
+    };
+    auto load = [&](Batch& bt, int b) {
         const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
             const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
 #pragma unroll
             for (int s = 0; s < SMAX; ++s)
-                if (s < S) fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, g[u][s]);
+                fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, bt.g[u][s]);
+        }
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int u = 0; u < RB; ++u) {
+                const int64_t ic = ib + u < row_end ? ib + u : row0;  // factor rows: clamped
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic * r, r, bt.ap[k][u]);
+            }
         }
     };
-    auto process = [&](Rows& g, int b) {
+    // segments past S load zeros (kOob) and drop their stores; their arithmetic is skipped
+    // by a uniform branch
+    auto seg_on = [&](int s) { return s < S; };
+    auto process = [&](Batch& bt, int b) {
         const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
         int64_t ic[RB];
 #pragma unroll
         for (int u = 0; u < RB; ++u) ic[u] = ib + u < row_end ? ib + u : row0;  // factor rows: clamped
-        float ap[KC][RB][R];
-        if constexpr (K > 0) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-#pragma unroll
-                for (int u = 0; u < RB; ++u)
-                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic[u] * r, r, ap[k][u]);
-        }
+        auto& g = bt.g;
+        auto& ap = bt.ap;
         float dot[RB][R];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
 #pragma unroll
             for (int s = 0; s < SMAX; ++s)
-                if (s < S) {
 #pragma unroll
-                    for (int v = 0; v < 4; ++v) keep(g[u][s][v]);
-                }
+                for (int v = 0; v < 4; ++v) keep(g[u][s][v]);
 #pragma unroll
             for (int c = 0; c < R; ++c) dot[u][c] = 0.f;
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                if (s < S) {
+                if (seg_on(s)) {
                     // error feedback of the earlier iterations (reference :195-202), same
                     // per-element arithmetic as the product and k_apply
                     if constexpr (K > 0) {
@@ -356,7 +375,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
             const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
-                if (s < S) {
+                if (seg_on(s)) {
                     float res[4], o[4];
                     float xs[4][R];
                     segx(s, xs);
@@ -399,15 +418,13 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     // synchronises and stores (the workgroup barrier no longer idles the memory system)
     const int64_t rows = row_end - row0;
     const int nb = int((rows + int64_t(RGS) * RB - 1) / (int64_t(RGS) * RB));
-    Rows ga, gb;
-    if (nb > 0) load(ga, 0);
+    Batch ga, gb;
+    load(ga, 0);
     for (int b = 0; b < nb; b += 2) {
-        if (b + 1 < nb) load(gb, b + 1);
+        load(gb, b + 1);
         process(ga, b);
-        if (b + 1 < nb) {
-            if (b + 2 < nb) load(ga, b + 2);
-            process(gb, b + 1);
-        }
+        load(ga, b + 2);
+        if (b + 1 < nb) process(gb, b + 1);
     }
 }
 

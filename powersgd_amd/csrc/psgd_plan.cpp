@@ -158,18 +158,38 @@ struct FinGeom {
 
 // Fused final odd pass (psgd_final.cuh): row groups of T threads (4 columns each, S
 // segments), fin_rb(R) rows per group per batch, blocks of about fin_elems elements.
-int fin_rb(int R) { return R == 4 ? 1 : 2; }   // == FinRB<R>
+#ifndef PSGD_FIN_RB12
+#define PSGD_FIN_RB12 2
+#endif
+int fin_rb(int R) { return R == 4 ? 1 : PSGD_FIN_RB12; }   // == FinRB<R>
 int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
 // the two kernel forms: register panels (k_final_odd) and LDS panels (k_final_lds)
 struct FinForm {
     int nt, tmax, rb;
 };
 FinForm fin_form(int R, bool lds) { return lds ? FinForm{1024, 512, 1} : FinForm{fin_nt(R), fin_nt(R), fin_rb(R)}; }
-FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems) {
+// scap = 0: the widest row group (T = min(tmax, 4-column units rounded up to a power of
+// two), fewest segments). scap > 0: the row group with the fewest idle lanes among
+// S <= scap (ties: the narrower group — more rows per batch and, at T <= 64, a row sum
+// within one wave instead of across waves through LDS); e.g. m = 576: T = 32, S = 5 (10 %
+// idle) rather than T = 256, S = 1 (44 % idle).
+FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int scap = 0) {
     FinGeom g;
     const int64_t q4 = (m + 3) / 4;
     g.T = int(std::min<int64_t>(f.tmax, pow2ceil(q4)));
     g.S = int((q4 + g.T - 1) / g.T);
+    if (scap > 0) {
+        int64_t best = int64_t(g.S) * g.T;
+        for (int T = g.T / 2; T >= 4; T /= 2) {
+            const int64_t S = (q4 + T - 1) / T;
+            if (S > scap) break;
+            if (S * T <= best) {
+                best = S * T;
+                g.T = T;
+                g.S = int(S);
+            }
+        }
+    }
     const int64_t batch = int64_t(f.nt / g.T) * f.rb;  // rows per workgroup batch
     int64_t rows = round_up(std::max<int64_t>(1, (fin_elems + m - 1) / m), batch);
     // a small matrix must still spread over several workgroups
@@ -352,9 +372,16 @@ struct psgd_plan {
         if (fin_ok) {
             const FinForm f = fin_form(rbucket, fin_lds);
             const int64_t elems = fin_lds ? fin_elems_lds : fin_elems;
+            // segments per row up to the kernel bucket the widest groups already need
+            // (at most 5: the exact-S bodies), for fewer idle lanes
+            int scap = 0;
+            if (env_int("PSGD_FIN_GEOM", 1) && !fin_lds) {
+                for (const MatDesc& d : mats) scap = std::max(scap, fin_geometry(d.n, d.m, f, 0).S);
+                scap = std::min(fin_bucket(scap), 5);
+            }
             for (size_t i = 0; i < mats.size(); ++i) {
                 MatDesc& d = mats[i];
-                const FinGeom fg = fin_geometry(d.n, d.m, f, elems);
+                const FinGeom fg = fin_geometry(d.n, d.m, f, elems, scap);
                 d.fin_T = fg.T;
                 d.fin_S = fg.S;
                 d.fin_rows = fg.rows;
@@ -618,8 +645,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
-        p->tiles_fin_cap += std::max(fin_geometry(md.n, md.m, fin_form(p->rbucket, false), p->fin_elems).ntiles,
-                                     fin_geometry(md.n, md.m, fin_form(p->rbucket, true), p->fin_elems_lds).ntiles);
+        int64_t cap = fin_geometry(md.n, md.m, fin_form(p->rbucket, true), p->fin_elems_lds).ntiles;
+        for (int sc = 0; sc <= 5; ++sc)  // any segment cap set_vec may pick
+            cap = std::max(cap, fin_geometry(md.n, md.m, fin_form(p->rbucket, false), p->fin_elems, sc).ntiles);
+        p->tiles_fin_cap += cap;
         if (i == 0 || p->mats[i - 1].group != md.group) {
             p->grng_even.push_back(int32_t(p->red_even.size()));
             p->grng_even.push_back(0);

@@ -907,39 +907,65 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
     }
     const float alpha = a.alpha;
 
-    for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
+    // batches of kUnroll rows: all gradient rows AND their error-feedback factor rows are
+    // loaded before the first is consumed (factor rows loaded inside the term loop were a
+    // chain of kUnroll dependent round trips per batch)
+    struct Batch {
         float x[kUnroll][V];
         int64_t rc[kUnroll];
+        float ap[NC][kUnroll][R];
+        float aa[NA][kUnroll][R];
+    };
+    auto load = [&](Batch& b, int64_t row) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
-            rc[u] = rr < g.row_end ? rr : g.row_begin;
-            Io<T>::ld(G + rc[u] * g.m + g.ccol, x[u]);
+            b.rc[u] = rr < g.row_end ? rr : g.row_begin;
+            Io<T>::ld(G + b.rc[u] * g.m + g.ccol, b.x[u]);
         }
+        if constexpr (NI > 0) {
+#pragma unroll
+            for (int k = 0; k < NI; ++k)
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const int32_t prow = int32_t(b.rc[u]) * r;
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, b.ap[k][u]);
+                    if constexpr (!SHARED) ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, b.aa[k][u]);
+                }
+        }
+    };
+    auto process = [&](Batch& b, int64_t row) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int32_t prow = int32_t(rc[u]) * r;
+            const int32_t prow = int32_t(b.rc[u]) * r;
             float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) o[v] = 0.f;
             for (int k = 0; k < nt; ++k) {
-                float ap[R];
-                ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
-                float aa[R];
-                if constexpr (!SHARED) ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, aa);
+                float ap[R], aa[R];
+                if constexpr (NI > 0) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c) {
+                        ap[c] = b.ap[k < NC ? k : 0][u][c];
+                        aa[c] = b.aa[k < NA ? k : 0][u][c];
+                    }
+                } else {
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
+                    if constexpr (!SHARED) ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, aa);
+                }
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                    float b[R];
+                    float bv[R];
                     if constexpr (NI > 0) {
 #pragma unroll
-                        for (int c = 0; c < R; ++c) b[c] = bq[k < NC ? k : 0][v][c];
+                        for (int c = 0; c < R; ++c) bv[c] = bq[k < NC ? k : 0][v][c];
                     } else {
-                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, b);
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bv);
                     }
-                    const float tk = dotr<R>(ap, b);
-                    x[u][v] = x[u][v] - tk;  // reference :195-202 (alpha = -1)
+                    const float tk = dotr<R>(ap, bv);
+                    b.x[u][v] = b.x[u][v] - tk;  // reference :195-202 (alpha = -1)
                     if constexpr (SHARED) {
-                        o[v] = o[v] + tk;    // world size 1: Qbar == Q_local, alpha = 1
+                        o[v] = o[v] + tk;        // world size 1: Qbar == Q_local, alpha = 1
                     } else {
                         float bb[R];
                         if constexpr (NI > 0) {
@@ -953,10 +979,15 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
                 }
             }
             if (g.active && row + u * g.stride < g.row_end) {
-                Io<T>::st(D + rc[u] * g.m + g.col0, x[u]);
-                Io<T>::st(O + rc[u] * g.m + g.col0, o);
+                Io<T>::st(D + b.rc[u] * g.m + g.col0, b.x[u]);
+                Io<T>::st(O + b.rc[u] * g.m + g.col0, o);
             }
         }
+    };
+    for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
+        Batch b;
+        load(b, row);
+        process(b, row);
     }
 }
 
