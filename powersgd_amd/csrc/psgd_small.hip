@@ -1239,12 +1239,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         if (wave != 0) return;
         const RedItem it = a.nitems[blockIdx.x - a.nmain];
         const MatDesc d = a.mats[it.mat];
-        const float dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
         const int64_t len = (a.even ? d.n : d.m) * d.r;
         const int64_t e = int64_t(it.start) + lane;
+        const int64_t i = (a.even ? d.poff : d.qoff) + (e < len ? e : 0);
+        float x = a.raw[i];  // in flight together with the norm's loads
+        const float dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
         if (e < len) {
-            const int64_t i = (a.even ? d.poff : d.qoff) + e;
-            const float x = a.raw[i] / dn;  // matrix.div_(max(norm, eps))
+            x = x / dn;  // matrix.div_(max(norm, eps))
             a.xstate[i] = x;
             a.hx[i] = x;
         }
@@ -1258,6 +1259,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     const int np = a.even ? d.nchunk : d.odd_nstrip;
     const int c0 = wave * np / kWaves, c1 = (wave + 1) * np / kWaves;
     const float* p = a.part + (a.even ? d.part_even : d.part_odd) + ec;
+    // wave 0's first group-norm loads go out before the partials' (group_norm_ss's order:
+    // lane-strided sums from 0, then the wave tree), so the two round trips overlap
+    const bool nrm = a.ss_in != nullptr && wave == 0;
+    int gb = 0, ge = 0;
+    float ssv = 0.f;
+    if (nrm) {
+        gb = a.grng_in[2 * d.group];
+        ge = a.grng_in[2 * d.group + 1];
+        ssv = gb + lane < ge ? a.ss_in[gb + lane] : 0.f;
+    }
     float s = 0.f;
     for (int c = c0; c < c1; c += 8) {  // loads issued 8 at a time (clamped, unconditional)
         float v[8];
@@ -1273,7 +1284,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     __syncthreads();
     if (wave != 0) return;
     s = ((red[lane] + red[kRedElems + lane]) + red[2 * kRedElems + lane]) + red[3 * kRedElems + lane];
-    if (a.ss_in) s = s / group_norm_ss(a.ss_in, a.grng_in, d.group);  // G^T (x / d) == (G^T x) / d up to rounding
+    if (nrm) {
+        for (int i = gb + lane + 64; i < ge; i += 64) ssv += a.ss_in[i];
+        const float nv = sqrtf(wave_allsum(ssv));
+        s = s / (nv > 1e-16f ? nv : 1e-16f);  // G^T (x / d) == (G^T x) / d up to rounding
+    }
     if (e < len) {
         const int64_t dst = (a.even ? d.qoff : d.poff) + e;
         a.yloc[dst] = s;

@@ -481,6 +481,11 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
     for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
         float x[kUnroll][V];
         int64_t rc[kUnroll];
+        // the rows' factor values (in-factor rows for the even product, error-feedback rows)
+        // are loaded together with the gradient rows: loaded inside the row loop they were a
+        // chain of kUnroll dependent round trips per batch
+        float xpu[EVEN ? kUnroll : 1][R];
+        float apu[KC][kUnroll][R];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
@@ -489,12 +494,26 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
+            const int32_t prow = int32_t(rc[u]) * r;
+            if constexpr (EVEN) ld_factor<R>(xp_base + prow, r, xpu[u]);
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, apu[k][u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
             const bool valid = g.active && (row + u * g.stride) < g.row_end;
             const int32_t prow = int32_t(rc[u]) * r;
             // error feedback of the previous iterations, formed on the fly
             for (int k = 0; k < nres; ++k) {
                 float ap[R];
-                ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
+                if constexpr (K > 0) {
+#pragma unroll
+                    for (int c = 0; c < R; ++c) ap[c] = apu[k < KC ? k : 0][u][c];
+                } else {
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
+                }
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     float b[R];
@@ -510,12 +529,10 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 #pragma unroll
             for (int v = 0; v < V; ++v) x[u][v] = valid ? x[u][v] : 0.f;
             if constexpr (EVEN) {
-                float xp[R];
-                ld_factor<R>(xp_base + prow, r, xp);
 #pragma unroll
                 for (int v = 0; v < V; ++v)
 #pragma unroll
-                    for (int c = 0; c < R; ++c) acc[v][c] = fmaf(x[u][v], xp[c], acc[v][c]);
+                    for (int c = 0; c < R; ++c) acc[v][c] = fmaf(x[u][v], xpu[u][c], acc[v][c]);
             } else {
                 float dot[R];
 #pragma unroll
