@@ -7,6 +7,8 @@ from powersgd_amd import _lib
 from powersgd_amd.reducers import _Codec
 
 SETS = {
+    "one (49152,512)": [(49152, 512)],
+    "one (5120,4608)": [(5120, 4608)],
     "m512  (2048,512)x24": [(2048, 512)] * 24,
     "m4608 (512,4608)x10": [(512, 4608)] * 10,
     "m576  (4096,576)x10": [(4096, 576)] * 10,

@@ -103,6 +103,76 @@ __global__ __launch_bounds__(256) void k_r1w2_chunk(v4f* __restrict__ g, v4f* __
     }
 }
 
+// the fused final pass's access pattern without its arithmetic: rows of m floats, row groups
+// of T lanes (4 columns each, S segments of 4T columns), RB rows per group per batch, 256
+// threads, `rows` rows per block; r1w2 on every element
+template <int S, int RB>
+__global__ __launch_bounds__(256) void k_r1w2_rows(float* __restrict__ g, float* __restrict__ out, int m, int T,
+                                                   int rows, int n) {
+    extern __shared__ float occ_rows[];  // dynamic LDS only caps blocks per CU
+    if (rows < 0) occ_rows[threadIdx.x] = 0.f;
+    const int tid = threadIdx.x, rg = tid / T, tt = tid - rg * T, RGS = 256 / T;
+    const long row0 = long(blockIdx.x) * rows;
+    for (int b = 0; b * RGS * RB < rows; ++b) {
+        v4f x[RB][S];
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const long row = row0 + (long(b) * RGS + rg) * RB + u;
+                const int c = (s * T + tt) * 4;
+                x[u][s] = (row < n && c < m) ? *(const v4f*)(g + row * m + c) : v4f{0, 0, 0, 0};
+            }
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const long row = row0 + (long(b) * RGS + rg) * RB + u;
+                const int c = (s * T + tt) * 4;
+                if (row < n && c < m) {
+                    const v4f o = x[u][s] * 0.5f;
+                    *(v4f*)(out + row * m + c) = o;
+                    *(v4f*)(g + row * m + c) = x[u][s] - o;
+                }
+            }
+    }
+}
+
+// the same pattern through buffer descriptors (the codec's loads/stores: raw buffer
+// b128 with 32-bit byte offsets, rsrc word 3 = 0x00020000)
+template <int S, int RB>
+__global__ __launch_bounds__(256) void k_r1w2_rows_buf(float* __restrict__ g, float* __restrict__ out, int m, int T,
+                                                       int rows, int n) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const int nbytes = int(long(n) * m * 4);
+    const __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(g, 0, nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(out, 0, nbytes, 0x00020000);
+    const int tid = threadIdx.x, rg = tid / T, tt = tid - rg * T, RGS = 256 / T;
+    const long row0 = long(blockIdx.x) * rows;
+    for (int b = 0; b * RGS * RB < rows; ++b) {
+        v4u x[RB][S];
+        unsigned off[RB][S];
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const long row = row0 + (long(b) * RGS + rg) * RB + u;
+                const int c = (s * T + tt) * 4;
+                off[u][s] = (row < n && c < m) ? unsigned((row * m + c) * 4) : 0x80000000u;
+                x[u][s] = __builtin_amdgcn_raw_buffer_load_b128(gs, off[u][s], 0, 0);
+            }
+#pragma unroll
+        for (int u = 0; u < RB; ++u)
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                v4f xv = __builtin_bit_cast(v4f, x[u][s]);
+                const v4f o = xv * 0.5f;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, o), os, off[u][s], 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, xv - o), gs, off[u][s], 0, 0);
+            }
+    }
+}
+
 #define CK(x)                                                              \
     do {                                                                   \
         hipError_t e_ = (x);                                               \
@@ -159,6 +229,55 @@ int main() {
         printf("r1w2 chunk %6ld KB grid %6d  %7.2f us  %6.0f GB/s\n", C * 16 / 1024, gr, t, 3 * bytes / t / 1e3);
         t = time_it([&] { k_r1w2_chunk<8><<<gr, 256>>>(g, o, n4, C); }, 50);
         printf("r1w2 chunk U8 %6ld KB grid %6d  %7.2f us  %6.0f GB/s\n", C * 16 / 1024, gr, t, 3 * bytes / t / 1e3);
+    }
+    {
+        // (n, m, T, S) as the final pass's geometry picks them, ~100 MB each
+        struct Case { int n, m, T, S; };
+        const Case cs[] = {{49152, 512, 32, 4}, {49152, 512, 128, 1}, {5120, 4608, 256, 5}, {40960, 576, 32, 5},
+                           {40960, 576, 256, 1}};
+        for (const Case& c : cs) {
+            for (int rows_blk : {16, 32, 64}) {
+                const int rgs = 256 / c.T;
+                const int rows = (rows_blk + 2 * rgs - 1) / (2 * rgs) * (2 * rgs);
+                const int gr = (c.n + rows - 1) / rows;
+                float* gf = (float*)g;
+                float* of = (float*)o;
+                float t = 0.f;
+                switch (c.S) {
+                    case 1: t = time_it([&] { k_r1w2_rows<1, 2><<<gr, 256>>>(gf, of, c.m, c.T, rows, c.n); }, 30); break;
+                    case 4: t = time_it([&] { k_r1w2_rows<4, 2><<<gr, 256>>>(gf, of, c.m, c.T, rows, c.n); }, 30); break;
+                    case 5: t = time_it([&] { k_r1w2_rows<5, 2><<<gr, 256>>>(gf, of, c.m, c.T, rows, c.n); }, 30); break;
+                }
+                CK(hipGetLastError());
+                const double nb = 3.0 * c.n * double(c.m) * 4;
+                printf("rows n %5d m %4d T %3d S %d rows/blk %3d grid %5d  %7.2f us  %6.0f GB/s\n", c.n, c.m, c.T, c.S,
+                       rows, gr, t, nb / t / 1e3);
+            }
+        }
+    }
+    {
+        float* gf = (float*)g;
+        float* of = (float*)o;
+        float t1 = time_it([&] { k_r1w2_rows_buf<4, 2><<<3072, 256>>>(gf, of, 512, 32, 16, 49152); }, 30);
+        float t2 = time_it([&] { k_r1w2_rows_buf<5, 2><<<320, 256>>>(gf, of, 4608, 256, 16, 5120); }, 30);
+        float t3 = time_it([&] { k_r1w2_rows<4, 2><<<3072, 256>>>(gf, of, 512, 32, 16, 49152); }, 30);
+        float t4 = time_it([&] { k_r1w2_rows<5, 2><<<320, 256>>>(gf, of, 4608, 256, 16, 5120); }, 30);
+        CK(hipGetLastError());
+        printf("rows buffer ops: m512 T32 S4 %6.0f GB/s   m4608 T256 S5 %6.0f GB/s (global: %6.0f %6.0f)\n",
+               3.0 * 49152 * 512 * 4 / t1 / 1e3, 3.0 * 5120 * 4608 * 4 / t2 / 1e3, 3.0 * 49152 * 512 * 4 / t3 / 1e3,
+               3.0 * 5120 * 4608 * 4 / t4 / 1e3);
+    }
+    CK(hipFuncSetAttribute((const void*)k_r1w2_rows<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CK(hipFuncSetAttribute((const void*)k_r1w2_rows<5, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (int bpc : {1, 2, 3}) {
+        const size_t lds = size_t(160 * 1024 / bpc - 1024);
+        float* gf = (float*)g;
+        float* of = (float*)o;
+        float t1 = time_it([&] { k_r1w2_rows<4, 2><<<3072, 256, lds>>>(gf, of, 512, 32, 16, 49152); }, 30);
+        float t2 = time_it([&] { k_r1w2_rows<5, 2><<<320, 256, lds>>>(gf, of, 4608, 256, 16, 5120); }, 30);
+        CK(hipGetLastError());
+        printf("rows %d waves/SIMD: m512 T32 S4 %6.0f GB/s   m4608 T256 S5 %6.0f GB/s\n", bpc,
+               3.0 * 49152 * 512 * 4 / t1 / 1e3, 3.0 * 5120 * 4608 * 4 / t2 / 1e3);
     }
     // occupancy: blocks (= waves per SIMD) per CU capped through dynamic LDS
     CK(hipFuncSetAttribute((const void*)k_r1w2_chunk<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

@@ -8,6 +8,8 @@ import torch
 from powersgd_amd import Config, PowerSGD
 
 SETS = {
+    "one (49152,512)": [(49152, 512)],
+    "one (5120,4608)": [(5120, 4608)],
     "m147  (4096,147)x42": [(4096, 147)] * 42,
     "m256  (1024,256)x96": [(1024, 256, 1, 1)] * 96,
     "m512  (2048,512)x24": [(2048, 512, 1, 1)] * 24,
