@@ -8,4 +8,4 @@ B="bench.py --config $cfg --steps 50 --warmup 5 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- python3 $B > "$out/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o fetch -- python3 $B > "$out/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o write -- python3 $B > "$out/write.log" 2>&1
-python3 tools/prof_summary.py "$out" > "$out/summary.txt"
+python3 tools/prof_summary.py "$out" --traffic "$cfg" > "$out/summary.txt"
