@@ -173,6 +173,7 @@ struct OrthArgs {
     float* state;        // in-factor state buffer, orthonormalised in place
     float* hx;           // history copy of the orthonormal in-factor
     float* save;         // if non-null: copy of the pre-orthonormalisation values
+    int32_t flags;       // diagnostics (PSGD_ORTH_DIAG): 1 = skip the Householder fallback
 };
 
 // Host-side launchers (psgd_kernels*.hip). Return hipError_t.

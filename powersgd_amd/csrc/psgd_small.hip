@@ -1131,11 +1131,246 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
         orth_chol_panel<R, 0>(a, u, redd, red, tau);
 }
 
+// ------------------------------------------- Cholesky-QR for ranks 9-16 on fp64 MFMA ----
+// Same algorithm and LAPACK sign reconstruction as k_orth_chol, restructured for a 16-column
+// panel, where per-thread r x r register arrays no longer fit:
+//  * Gram G = X^T X with v_mfma_f64_16x16x4_f64: a wave loads 4 rows x 16 columns (lane
+//    l = X[row0 + l/16][l%16]); that one value is both the A operand (A[i][kk] = X[kk][i])
+//    and the B operand (B[kk][j] = X[kk][j]), so each row is read once and the matrix core
+//    forms all 256 products. 16 waves accumulate their own rows; partials summed via LDS in
+//    a fixed order (bitwise reproducible).
+//  * The 16 x 16 chain (Cholesky, R^-1, the signs' LU recursion on the top block) runs on
+//    wave 0 with lane-parallel LDS updates.
+//  * Y = X M' (M' = R^-1 D) again on the matrix core, transposed: D[c'][rr] = sum M'[l][c]
+//    X[row0+rr][l] with a column permutation c = pi(c'); lane l loads X[row0 + l%16][4(l/16)
+//    .. +3] (one 16-B load) and writes Y[row0 + l%16][4(l/16) .. +3].
+//  * v_mfma_f64_16x16x4_f64 layouts (cdna_hip_programming.md): A[i][k] in lane i + 16k,
+//    B[k][j] in lane j + 16k, D[i][j] in lane j + 16 (i % 4), item i / 4.
+// Columns >= r (a narrower matrix in the rank-16 bucket) are zero in X and identity in the
+// padded Gram, so they do not disturb the first r columns.
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+constexpr int kC16NT = 512;
+constexpr int kC16W = kC16NT / 64;
+
+__device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+__global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
+    constexpr int R = 16;
+    __shared__ double gsh[kC16W * 256];  // per-wave Gram partials (MFMA D layout)
+    __shared__ double wsh[256];          // G, then R (upper, row-major)
+    __shared__ double msh[256];          // M' = R^-1 D (row-major M'[l][c])
+    __shared__ double tsh[256];          // top block T = X[0:r] R^-1
+    __shared__ double xsh[256];          // top block of X
+    __shared__ double gdiag[R];
+    __shared__ double rd[kC16W];
+    __shared__ float red[kC16W * R];
+    __shared__ float tau[R];
+    __shared__ int ok_sh;
+    const OrthUnit u = a.units[blockIdx.x];
+    if (u.r == 1) {  // rank-1 group of a mixed-rank plan: the reference's joint norm
+        orth_joint_norm<kC16NT>(a, u, rd);
+        return;
+    }
+    const int r = u.r;
+    const int64_t k = u.k;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ri = lane & 15, kq = lane >> 4;
+    float* __restrict__ st = a.state + u.off;
+    float* __restrict__ hx = a.hx + u.off;
+    float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
+    const bool cv = ri < r;
+    const int cc = cv ? ri : 0;
+
+    // ---- Gram: wave w takes row quads w, w + 16, ...; kG quads per batch, loads in flight
+    constexpr int kG = 12;
+    f64x4_t g = {0.0, 0.0, 0.0, 0.0};
+    const int64_t nq = (k + 3) >> 2;
+    for (int64_t q0 = wave; q0 < nq; q0 += int64_t(kG) * kC16W) {
+        float v[kG];
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int64_t row = (q0 + int64_t(q) * kC16W) * 4 + kq;
+            v[q] = st[(row < k ? row : 0) * r + cc];
+        }
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int64_t row = (q0 + int64_t(q) * kC16W) * 4 + kq;
+            keep(v[q]);
+            const bool ok = cv && row < k;
+            v[q] = ok ? v[q] : 0.f;
+            if (sv && ok) sv[row * r + ri] = v[q];
+            g = __builtin_amdgcn_mfma_f64_16x16x4f64(double(v[q]), double(v[q]), g, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gsh[wave * 256 + e * 64 + lane] = g[e];
+    __syncthreads();
+    if (tid < 256) {  // fixed-order sum over waves; f64 D layout: D[(l>>4) + 4e][l&15]
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kC16W; ++w) s += gsh[w * 256 + tid];
+        const int e = tid >> 6, l = tid & 63;
+        const int i = (l >> 4) + 4 * e, j = l & 15;
+        if (i >= r || j >= r) s = (i == j) ? 1.0 : 0.0;  // identity padding
+        wsh[i * R + j] = s;
+        if (i == j) gdiag[i] = s;
+    }
+    __syncthreads();
+
+    if (wave == 0) {
+        // top block of X (rows 0..r-1), in flight during the factorisation
+        float xt[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = lane + 64 * q, i = e >> 4, l = e & 15;
+            xt[q] = st[(i < r ? i : 0) * r + (l < r ? l : 0)];
+        }
+        // Cholesky G = R^T R (upper R in place), lane-parallel trailing updates
+        bool ok = true;
+        for (int j = 0; j < R; ++j) {
+            lds_fence();
+            const double piv = wsh[j * R + j];
+            ok = ok && (j >= r || (piv > 1e-8 * gdiag[j] && piv > 0.0));
+            const double d = sqrt(piv > 0.0 ? piv : 1.0);
+            lds_fence();
+            if (lane < R && lane > j) wsh[j * R + lane] = wsh[j * R + lane] / d;
+            if (lane == j) wsh[j * R + j] = d;
+            lds_fence();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = lane + 64 * q, i = e >> 4, b = e & 15;
+                if (i > j && b >= i) wsh[e] = wsh[e] - wsh[j * R + i] * wsh[j * R + b];
+            }
+        }
+        lds_fence();
+        // M = R^-1: lane c owns column c (back substitution)
+        if (lane < R) {
+            const int c = lane;
+            double mc[R];
+#pragma unroll
+            for (int i = R - 1; i >= 0; --i) {
+                double v = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+                for (int l = i + 1; l < R; ++l) v -= wsh[i * R + l] * mc[l];
+                mc[i] = v / wsh[i * R + i];
+            }
+#pragma unroll
+            for (int i = 0; i < R; ++i) msh[i * R + c] = (i < r && c < r) ? mc[i] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            keep(xt[q]);
+            const int e = lane + 64 * q, i = e >> 4, l = e & 15;
+            xsh[e] = (i < r && l < r) ? double(xt[q]) : 0.0;
+        }
+        lds_fence();
+        // T = X[0:r] M
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = lane + 64 * q, i = e >> 4, c = e & 15;
+            double v = 0.0;
+#pragma unroll
+            for (int l = 0; l < R; ++l) v += xsh[i * R + l] * msh[l * R + c];
+            tsh[e] = v;
+        }
+        // LAPACK's column signs: the LU recursion of k_orth_chol, lane-parallel
+        double sg = 1.0;  // lane c < r ends with sgn[c]
+        for (int j = 0; j < r; ++j) {
+            lds_fence();
+            const double tjj = tsh[j * R + j];
+            const bool nonneg = tjj >= 0.0;
+            const double sj = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
+            if (lane == j) sg = sj;
+            const double piv = tjj - sj;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = lane + 64 * q, i = e >> 4, b = e & 15;
+                if (i > j && i < r && b > j && b < r) tsh[e] = tsh[e] - (tsh[i * R + j] / piv) * tsh[j * R + b];
+            }
+        }
+        lds_fence();
+        if (lane < R) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) msh[i * R + lane] = msh[i * R + lane] * sg;
+        }
+        if (lane == 0) ok_sh = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (!ok_sh && !(a.flags & 1)) {  // exact Householder (geqr2 + org2r) in place in hx
+        for (int64_t i = tid; i < k * r; i += kC16NT) hx[i] = st[i];
+        __syncthreads();
+        householder_q<R, kC16NT>(hx, k, r, red, tau);
+        for (int64_t i = tid; i < k * r; i += kC16NT) st[i] = hx[i];
+        return;
+    }
+
+    // ---- Y = X M' on the matrix core: 16-row blocks, wave w takes blocks w, w + 16, ...
+    // A_q[i = ri][kk = kq] = M'[4 kq + q][pi(ri)], pi(i) = 4 (i & 3) + (i >> 2): the f64 D
+    // layout puts row (l>>4) + 4e in lane l, item e, so this output-column permutation hands
+    // lane l the four contiguous columns 4 kq .. 4 kq + 3 of its row
+    double am[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) am[q] = msh[(4 * kq + q) * R + 4 * (ri & 3) + (ri >> 2)];
+    __syncthreads();  // the top block was read (wave 0) before any row is overwritten
+    constexpr int kA = 6;
+    const int64_t nb = (k + 15) >> 4;
+    // 16-B rows: one load per lane per block (state offsets of a mixed-rank plan need not
+    // be multiples of 4 floats)
+    const bool vec = r == R && ((reinterpret_cast<uintptr_t>(st) | reinterpret_cast<uintptr_t>(hx)) & 15) == 0;
+    for (int64_t b0 = wave; b0 < nb; b0 += int64_t(kA) * kC16W) {
+        float x[kA][4];
+#pragma unroll
+        for (int q = 0; q < kA; ++q) {
+            const int64_t row = (b0 + int64_t(q) * kC16W) * 16 + ri;
+            const int64_t rc = row < k ? row : 0;
+            if (vec) {
+                const float4 t = *reinterpret_cast<const float4*>(st + rc * R + 4 * kq);
+                x[q][0] = t.x; x[q][1] = t.y; x[q][2] = t.z; x[q][3] = t.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int c = 4 * kq + e;
+                    x[q][e] = st[rc * r + (c < r ? c : 0)];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kA; ++q) {
+            const int64_t row = (b0 + int64_t(q) * kC16W) * 16 + ri;
+            f64x4_t y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                keep(x[q][e]);
+                const float xv = (4 * kq + e < r) ? x[q][e] : 0.f;
+                y = __builtin_amdgcn_mfma_f64_16x16x4f64(am[e], double(xv), y, 0, 0, 0);
+            }
+            // lane l holds D[kq + 4e][ri] = Y[row0 + ri][pi(kq + 4e) = 4 kq + e]
+            if (row < k) {
+                if (vec) {
+                    const float4 o = make_float4(float(y[0]), float(y[1]), float(y[2]), float(y[3]));
+                    *reinterpret_cast<float4*>(st + row * R + 4 * kq) = o;
+                    *reinterpret_cast<float4*>(hx + row * R + 4 * kq) = o;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int c = 4 * kq + e;
+                        if (c < r) {
+                            st[row * r + c] = float(y[e]);
+                            hx[row * r + c] = float(y[e]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
 hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s) {
     switch (R) {
         case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
         case 4: k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a); break;
         case 8: k_orth_chol<8><<<nunits, CholNT<8>::value, 0, s>>>(a); break;
+        case 16: k_orth_chol16<<<nunits, kC16NT, 0, s>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1208,7 +1443,15 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipSt
         const char* e = std::getenv("PSGD_ORTH_CHOL");
         return !e || std::atoi(e) != 0;
     }();
-    if (chol && R <= 8) return launch_orth_chol(a, nunits, R, s);
+    static const int diag = [] {
+        const char* e = std::getenv("PSGD_ORTH_DIAG");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (chol && R <= 16) {
+        OrthArgs b = a;
+        b.flags = diag;
+        return launch_orth_chol(b, nunits, R, s);
+    }
     hipError_t err = hipSuccess;
     if (env_orth_wy() && launch_orth_wy(a, nunits, R, kmax, s, &err)) return err;
     if (rpt <= 16 && orth_reg_ok(R, int(rpt))) {
