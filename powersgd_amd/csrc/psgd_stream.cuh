@@ -1073,8 +1073,11 @@ hipError_t dispatch_product(int R, bool even, int nres, const ProductArgs& a, in
 template <typename T, int R>
 hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s) {
     const dim3 grid(ntiles + a.flat.nitems), block(kBlock);
-    constexpr bool kCache = R <= 8;
-    const int NI = (kCache && nterms <= 4) ? nterms : -1;
+    // register-cached factor terms: up to 4 at ranks <= 8, up to 2 at rank 16 (I <= 2);
+    // wider ranks load factor rows per element
+    constexpr bool kCache = R <= 16;
+    constexpr int kMaxNI = R <= 8 ? 4 : 2;
+    const int NI = (kCache && nterms <= kMaxNI) ? nterms : -1;
 #define PSGD_A(NN)                                                                       \
     do {                                                                                 \
         if (shared)                                                                      \
@@ -1082,12 +1085,18 @@ hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int nti
         else                                                                             \
             k_apply<T, R, NN, false><<<grid, block, 0, s>>>(a);                          \
     } while (0)
-    if constexpr (kCache) {
+    if constexpr (kCache && kMaxNI == 4) {
         switch (NI) {
             case 1: PSGD_A(1); break;
             case 2: PSGD_A(2); break;
             case 3: PSGD_A(3); break;
             case 4: PSGD_A(4); break;
+            default: PSGD_A(-1); break;
+        }
+    } else if constexpr (kCache) {
+        switch (NI) {
+            case 1: PSGD_A(1); break;
+            case 2: PSGD_A(2); break;
             default: PSGD_A(-1); break;
         }
     } else {
