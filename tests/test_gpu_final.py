@@ -120,7 +120,7 @@ def test_fused_final_bf16():
         assert _rel(g[i].float(), g_c[i], x[i]) <= 1e-2
 
 
-@pytest.mark.parametrize("rank,iters", [(1, 2), (2, 2), (1, 1)])
+@pytest.mark.parametrize("rank,iters", [(1, 2), (2, 2), (1, 1), (16, 2)])
 def test_split_calls_match_aggregate(rank, iters):
     """psgd_compress (fused last iteration writes the residual) + psgd_decompress
     (k_lowrank_out writes the output): the world-size > 1 sequence, at world size 1."""

@@ -218,3 +218,30 @@ def test_orthonormal_in_factor_every_rank_bucket(rank):
     oc = O.policy_step(ora, [g.cpu() for g in orig])
     for i, g in enumerate(orig):
         assert _rel(outs[i], oc[i], g) <= TOL_STEP, (rank, i, _rel(outs[i], oc[i], g))
+
+
+@pytest.mark.parametrize("rank,iters", [(12, 2), (16, 2), (16, 3)])
+def test_wide_rank_free_running(rank, iters):
+    """Ranks 9-16: k_orth_chol16 (fp64 MFMA Cholesky-QR) and k_apply with register-cached
+    terms (I = 2) or per-element factor loads (I = 3), two free-running steps with error
+    feedback against the oracle from the same initial state."""
+    shapes = [(300, 200), (64, 1000), (1000, 64), (128, 8, 3, 3), (40,)]
+    params = [torch.zeros(s, device=DEV) for s in shapes]
+    psgd = PowerSGD(params, Config(rank, 0.1, iters, 0))
+    ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 0.1, iters, 0)
+    ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
+    ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+    res_d = [torch.zeros(s, device=DEV) for s in shapes]
+    res_c = [torch.zeros(s) for s in shapes]
+    for t in range(2):
+        new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=60 + t)]
+        gd = [r + x.to(DEV) for r, x in zip(res_d, new)]
+        gc = [r + x for r, x in zip(res_c, new)]
+        scale = [g.cpu().clone() for g in gc]
+        od = psgd.aggregate(gd)
+        oc = O.policy_step(ora, gc)
+        torch.cuda.synchronize()
+        for i, g in enumerate(scale):
+            assert _rel(od[i], oc[i], g) <= TOL_FREE, (t, i, "out", _rel(od[i], oc[i], g))
+            assert _rel(gd[i], gc[i], g) <= TOL_FREE, (t, i, "res", _rel(gd[i], gc[i], g))
+        res_d, res_c = gd, gc
