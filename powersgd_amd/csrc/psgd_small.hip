@@ -1154,18 +1154,27 @@ constexpr int kC16W = kC16NT / 64;
 
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
-__global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
-    constexpr int R = 16;
-    __shared__ double gsh[kC16W * 256];  // per-wave Gram partials (MFMA D layout)
-    __shared__ double wsh[256];          // G, then R (upper, row-major)
-    __shared__ double msh[256];          // M' = R^-1 D (row-major M'[l][c])
-    __shared__ double tsh[256];          // top block T = X[0:r] R^-1
-    __shared__ double xsh[256];          // top block of X
+// R = 16 or 32: NB = R / 16 column blocks of 16; the Gram is NB (NB + 1) / 2 MFMA blocks
+// (upper), the apply NB x NB blocks of four MFMAs.
+template <int R>
+__device__ __forceinline__ void orth_chol_wide(const OrthArgs& a) {
+    constexpr int NB = R / 16;
+    constexpr int NBLK = NB * (NB + 1) / 2;
+    constexpr int RR = R * R;
+    constexpr int PER = RR / 64;  // r x r entries per lane of wave 0
+    // per-wave Gram partials; after the wave sum the same storage holds M', T and X's top block
+    constexpr int kScratch = (kC16W * NBLK * 256 > 3 * RR) ? kC16W * NBLK * 256 : 3 * RR;
+    __shared__ double scratch[kScratch];
+    __shared__ double wsh[RR];  // G, then R (upper, row-major)
     __shared__ double gdiag[R];
     __shared__ double rd[kC16W];
     __shared__ float red[kC16W * R];
     __shared__ float tau[R];
     __shared__ int ok_sh;
+    double* gsh = scratch;
+    double* msh = scratch;           // M' = R^-1 D (row-major M'[l][c])
+    double* tsh = scratch + RR;      // top block T = X[0:r] R^-1
+    double* xsh = scratch + 2 * RR;  // top block of X
     const OrthUnit u = a.units[blockIdx.x];
     if (u.r == 1) {  // rank-1 group of a mixed-rank plan: the reference's joint norm
         orth_joint_norm<kC16NT>(a, u, rd);
@@ -1178,51 +1187,72 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
     float* __restrict__ st = a.state + u.off;
     float* __restrict__ hx = a.hx + u.off;
     float* __restrict__ sv = a.save ? a.save + u.off : nullptr;
-    const bool cv = ri < r;
-    const int cc = cv ? ri : 0;
 
     // ---- Gram: wave w takes row quads w, w + 16, ...; kG quads per batch, loads in flight
-    constexpr int kG = 12;
-    f64x4_t g = {0.0, 0.0, 0.0, 0.0};
+    constexpr int kG = NB == 1 ? 12 : 6;
+    f64x4_t g[NBLK];
+#pragma unroll
+    for (int bl = 0; bl < NBLK; ++bl) g[bl] = f64x4_t{0.0, 0.0, 0.0, 0.0};
     const int64_t nq = (k + 3) >> 2;
     for (int64_t q0 = wave; q0 < nq; q0 += int64_t(kG) * kC16W) {
-        float v[kG];
+        float v[kG][NB];
 #pragma unroll
         for (int q = 0; q < kG; ++q) {
             const int64_t row = (q0 + int64_t(q) * kC16W) * 4 + kq;
-            v[q] = st[(row < k ? row : 0) * r + cc];
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) {
+                const int c = 16 * cb + ri;
+                v[q][cb] = st[(row < k ? row : 0) * r + (c < r ? c : 0)];
+            }
         }
 #pragma unroll
         for (int q = 0; q < kG; ++q) {
             const int64_t row = (q0 + int64_t(q) * kC16W) * 4 + kq;
-            keep(v[q]);
-            const bool ok = cv && row < k;
-            v[q] = ok ? v[q] : 0.f;
-            if (sv && ok) sv[row * r + ri] = v[q];
-            g = __builtin_amdgcn_mfma_f64_16x16x4f64(double(v[q]), double(v[q]), g, 0, 0, 0);
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) {
+                keep(v[q][cb]);
+                const int c = 16 * cb + ri;
+                const bool ok = c < r && row < k;
+                v[q][cb] = ok ? v[q][cb] : 0.f;
+                if (sv && ok) sv[row * r + c] = v[q][cb];
+            }
+            int bl = 0;
+#pragma unroll
+            for (int ca = 0; ca < NB; ++ca)
+#pragma unroll
+                for (int cb = ca; cb < NB; ++cb) {
+                    g[bl] = __builtin_amdgcn_mfma_f64_16x16x4f64(double(v[q][ca]), double(v[q][cb]), g[bl], 0, 0, 0);
+                    ++bl;
+                }
         }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) gsh[wave * 256 + e * 64 + lane] = g[e];
+    for (int bl = 0; bl < NBLK; ++bl)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gsh[(wave * NBLK + bl) * 256 + e * 64 + lane] = g[bl][e];
     __syncthreads();
-    if (tid < 256) {  // fixed-order sum over waves; f64 D layout: D[(l>>4) + 4e][l&15]
+    for (int t = tid; t < NBLK * 256; t += kC16NT) {  // fixed-order wave sum; f64 D layout
+        const int bl = t >> 8, el = t & 255;
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kC16W; ++w) s += gsh[w * 256 + tid];
-        const int e = tid >> 6, l = tid & 63;
-        const int i = (l >> 4) + 4 * e, j = l & 15;
+        for (int w = 0; w < kC16W; ++w) s += gsh[(w * NBLK + bl) * 256 + el];
+        int ca = 0, cb = 0, x = bl;  // block index -> (ca <= cb)
+        while (x >= NB - ca) { x -= NB - ca; ++ca; }
+        cb = ca + x;
+        const int e = el >> 6, l = el & 63;
+        const int i = 16 * ca + (l >> 4) + 4 * e, j = 16 * cb + (l & 15);
         if (i >= r || j >= r) s = (i == j) ? 1.0 : 0.0;  // identity padding
         wsh[i * R + j] = s;
         if (i == j) gdiag[i] = s;
     }
-    __syncthreads();
+    __syncthreads();  // gsh is dead from here on (msh / tsh / xsh reuse it)
 
     if (wave == 0) {
         // top block of X (rows 0..r-1), in flight during the factorisation
-        float xt[4];
+        float xt[PER];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = lane + 64 * q, i = e >> 4, l = e & 15;
+        for (int q = 0; q < PER; ++q) {
+            const int e = lane + 64 * q, i = e / R, l = e % R;
             xt[q] = st[(i < r ? i : 0) * r + (l < r ? l : 0)];
         }
         // Cholesky G = R^T R (upper R in place), lane-parallel trailing updates
@@ -1236,40 +1266,38 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
             if (lane < R && lane > j) wsh[j * R + lane] = wsh[j * R + lane] / d;
             if (lane == j) wsh[j * R + j] = d;
             lds_fence();
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int e = lane + 64 * q, i = e >> 4, b = e & 15;
+#pragma unroll 4
+            for (int q = 0; q < PER; ++q) {
+                const int e = lane + 64 * q, i = e / R, b = e % R;
                 if (i > j && b >= i) wsh[e] = wsh[e] - wsh[j * R + i] * wsh[j * R + b];
             }
         }
         lds_fence();
-        // M = R^-1: lane c owns column c (back substitution)
+        // M = R^-1: lane c owns column c (back substitution; the column lives in LDS, where
+        // only lane c touches it, so no register array of R doubles is needed)
         if (lane < R) {
             const int c = lane;
-            double mc[R];
-#pragma unroll
             for (int i = R - 1; i >= 0; --i) {
                 double v = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-                for (int l = i + 1; l < R; ++l) v -= wsh[i * R + l] * mc[l];
-                mc[i] = v / wsh[i * R + i];
+                for (int l = i + 1; l < R; ++l) v -= wsh[i * R + l] * msh[l * R + c];
+                msh[i * R + c] = v / wsh[i * R + i];
             }
-#pragma unroll
-            for (int i = 0; i < R; ++i) msh[i * R + c] = (i < r && c < r) ? mc[i] : 0.0;
+            for (int i = 0; i < R; ++i)
+                if (i >= r || c >= r) msh[i * R + c] = 0.0;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < PER; ++q) {
             keep(xt[q]);
-            const int e = lane + 64 * q, i = e >> 4, l = e & 15;
+            const int e = lane + 64 * q, i = e / R, l = e % R;
             xsh[e] = (i < r && l < r) ? double(xt[q]) : 0.0;
         }
         lds_fence();
         // T = X[0:r] M
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = lane + 64 * q, i = e >> 4, c = e & 15;
+#pragma unroll 1
+        for (int q = 0; q < PER; ++q) {
+            const int e = lane + 64 * q, i = e / R, c = e % R;
             double v = 0.0;
-#pragma unroll
+#pragma unroll 16
             for (int l = 0; l < R; ++l) v += xsh[i * R + l] * msh[l * R + c];
             tsh[e] = v;
         }
@@ -1282,9 +1310,9 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
             const double sj = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
             if (lane == j) sg = sj;
             const double piv = tjj - sj;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int e = lane + 64 * q, i = e >> 4, b = e & 15;
+#pragma unroll 4
+            for (int q = 0; q < PER; ++q) {
+                const int e = lane + 64 * q, i = e / R, b = e % R;
                 if (i > j && i < r && b > j && b < r) tsh[e] = tsh[e] - (tsh[i * R + j] / piv) * tsh[j * R + b];
             }
         }
@@ -1305,58 +1333,76 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
     }
 
     // ---- Y = X M' on the matrix core: 16-row blocks, wave w takes blocks w, w + 16, ...
-    // A_q[i = ri][kk = kq] = M'[4 kq + q][pi(ri)], pi(i) = 4 (i & 3) + (i >> 2): the f64 D
-    // layout puts row (l>>4) + 4e in lane l, item e, so this output-column permutation hands
-    // lane l the four contiguous columns 4 kq .. 4 kq + 3 of its row
-    double am[4];
+    // Output block cb, inner block lb, MFMA e covers inner columns l = 16 lb + 4 kk + e:
+    // A[i = ri][kk = kq] = M'[16 lb + 4 kq + e][16 cb + pi(ri)], pi(i) = 4 (i & 3) + (i >> 2):
+    // the f64 D layout puts row (l>>4) + 4e in lane l, item e, so this output-column
+    // permutation hands lane l the four contiguous columns 16 cb + 4 kq .. + 3 of its row
+    double am[NB][NB][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) am[q] = msh[(4 * kq + q) * R + 4 * (ri & 3) + (ri >> 2)];
+    for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+        for (int lb = 0; lb < NB; ++lb)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                am[cb][lb][e] = msh[(16 * lb + 4 * kq + e) * R + 16 * cb + 4 * (ri & 3) + (ri >> 2)];
     __syncthreads();  // the top block was read (wave 0) before any row is overwritten
-    constexpr int kA = 6;
+    constexpr int kA = NB == 1 ? 6 : 3;
     const int64_t nb = (k + 15) >> 4;
-    // 16-B rows: one load per lane per block (state offsets of a mixed-rank plan need not
-    // be multiples of 4 floats)
+    // 16-B rows: one load per lane per block and column block (state offsets of a
+    // mixed-rank plan need not be multiples of 4 floats)
     const bool vec = r == R && ((reinterpret_cast<uintptr_t>(st) | reinterpret_cast<uintptr_t>(hx)) & 15) == 0;
     for (int64_t b0 = wave; b0 < nb; b0 += int64_t(kA) * kC16W) {
-        float x[kA][4];
+        float x[kA][NB][4];
 #pragma unroll
         for (int q = 0; q < kA; ++q) {
             const int64_t row = (b0 + int64_t(q) * kC16W) * 16 + ri;
             const int64_t rc = row < k ? row : 0;
-            if (vec) {
-                const float4 t = *reinterpret_cast<const float4*>(st + rc * R + 4 * kq);
-                x[q][0] = t.x; x[q][1] = t.y; x[q][2] = t.z; x[q][3] = t.w;
-            } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int c = 4 * kq + e;
-                    x[q][e] = st[rc * r + (c < r ? c : 0)];
+            for (int lb = 0; lb < NB; ++lb) {
+                if (vec) {
+                    const float4 t = *reinterpret_cast<const float4*>(st + rc * R + 16 * lb + 4 * kq);
+                    x[q][lb][0] = t.x; x[q][lb][1] = t.y; x[q][lb][2] = t.z; x[q][lb][3] = t.w;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int c = 16 * lb + 4 * kq + e;
+                        x[q][lb][e] = st[rc * r + (c < r ? c : 0)];
+                    }
                 }
             }
         }
 #pragma unroll
         for (int q = 0; q < kA; ++q) {
             const int64_t row = (b0 + int64_t(q) * kC16W) * 16 + ri;
-            f64x4_t y = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                keep(x[q][e]);
-                const float xv = (4 * kq + e < r) ? x[q][e] : 0.f;
-                y = __builtin_amdgcn_mfma_f64_16x16x4f64(am[e], double(xv), y, 0, 0, 0);
-            }
-            // lane l holds D[kq + 4e][ri] = Y[row0 + ri][pi(kq + 4e) = 4 kq + e]
-            if (row < k) {
-                if (vec) {
-                    const float4 o = make_float4(float(y[0]), float(y[1]), float(y[2]), float(y[3]));
-                    *reinterpret_cast<float4*>(st + row * R + 4 * kq) = o;
-                    *reinterpret_cast<float4*>(hx + row * R + 4 * kq) = o;
-                } else {
+            for (int lb = 0; lb < NB; ++lb)
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int c = 4 * kq + e;
-                        if (c < r) {
-                            st[row * r + c] = float(y[e]);
-                            hx[row * r + c] = float(y[e]);
+                for (int e = 0; e < 4; ++e) {
+                    keep(x[q][lb][e]);
+                    x[q][lb][e] = (16 * lb + 4 * kq + e < r) ? x[q][lb][e] : 0.f;
+                }
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) {
+                f64x4_t y = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int lb = 0; lb < NB; ++lb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        y = __builtin_amdgcn_mfma_f64_16x16x4f64(am[cb][lb][e], double(x[q][lb][e]), y, 0, 0, 0);
+                // lane l holds D[kq + 4e][ri] = Y[row0 + ri][16 cb + pi(kq + 4e) = 16 cb + 4 kq + e]
+                if (row < k) {
+                    if (vec) {
+                        const float4 o = make_float4(float(y[0]), float(y[1]), float(y[2]), float(y[3]));
+                        *reinterpret_cast<float4*>(st + row * R + 16 * cb + 4 * kq) = o;
+                        *reinterpret_cast<float4*>(hx + row * R + 16 * cb + 4 * kq) = o;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int c = 16 * cb + 4 * kq + e;
+                            if (c < r) {
+                                st[row * r + c] = float(y[e]);
+                                hx[row * r + c] = float(y[e]);
+                            }
                         }
                     }
                 }
@@ -1365,12 +1411,16 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) {
     }
 }
 
+__global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) { orth_chol_wide<16>(a); }
+__global__ __launch_bounds__(kC16NT) void k_orth_chol32(OrthArgs a) { orth_chol_wide<32>(a); }
+
 hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s) {
     switch (R) {
         case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
         case 4: k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a); break;
         case 8: k_orth_chol<8><<<nunits, CholNT<8>::value, 0, s>>>(a); break;
         case 16: k_orth_chol16<<<nunits, kC16NT, 0, s>>>(a); break;
+        case 32: k_orth_chol32<<<nunits, kC16NT, 0, s>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1447,7 +1497,7 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipSt
         const char* e = std::getenv("PSGD_ORTH_DIAG");
         return e ? std::atoi(e) : 0;
     }();
-    if (chol && R <= 16) {
+    if (chol && R <= 32) {
         OrthArgs b = a;
         b.flags = diag;
         return launch_orth_chol(b, nunits, R, s);

@@ -21,7 +21,7 @@ DEV = torch.device("cuda:0")
 SHAPES = [(64, 64), (300, 8, 3, 3), (8, 8), (1024, 256), (96, 4608), (5, 700), (2048, 512)]
 
 
-@pytest.mark.parametrize("rank", [2, 3, 4, 5, 8, 12, 16])
+@pytest.mark.parametrize("rank", [2, 3, 4, 5, 8, 12, 16, 24, 32])
 @pytest.mark.parametrize("chol", ["1", "0"])
 def test_state_signs_match_lapack(rank, chol):
     old = os.environ.get("PSGD_ORTH_CHOL")
@@ -45,7 +45,7 @@ def test_state_signs_match_lapack(rank, chol):
             os.environ["PSGD_ORTH_CHOL"] = old
 
 
-@pytest.mark.parametrize("rank", [2, 4, 16])
+@pytest.mark.parametrize("rank", [2, 4, 16, 32])
 def test_zero_and_rank_deficient_panels(rank):
     """Zero gradients make the next factor zero (Householder fallback: identity columns);
     a rank-1 gradient makes it rank deficient."""

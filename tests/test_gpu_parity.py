@@ -220,9 +220,9 @@ def test_orthonormal_in_factor_every_rank_bucket(rank):
         assert _rel(outs[i], oc[i], g) <= TOL_STEP, (rank, i, _rel(outs[i], oc[i], g))
 
 
-@pytest.mark.parametrize("rank,iters", [(12, 2), (16, 2), (16, 3)])
+@pytest.mark.parametrize("rank,iters", [(12, 2), (16, 2), (16, 3), (32, 2)])
 def test_wide_rank_free_running(rank, iters):
-    """Ranks 9-16: k_orth_chol16 (fp64 MFMA Cholesky-QR) and k_apply with register-cached
+    """Ranks 9-32: k_orth_chol16/32 (fp64 MFMA Cholesky-QR) and k_apply with register-cached
     terms (I = 2) or per-element factor loads (I = 3), two free-running steps with error
     feedback against the oracle from the same initial state."""
     shapes = [(300, 200), (64, 1000), (1000, 64), (128, 8, 3, 3), (40,)]
