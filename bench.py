@@ -1,20 +1,30 @@
 """Benchmark of the PowerSGD hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config NAME] [--sets S]
 
 One step = one ``PowerSGD.aggregate`` over the synthetic gradients of the workload
 (compressed matrices: power iterations + factor all-reduce + fused residual/output
 pass; uncompressed tensors: flat pack + all-reduce), inputs resident in HBM.
-N > 1: one process per GPU (torch.distributed.run), every rank holds its own gradients
-(data parallel, weak scaling) and the P/Q factors are SUM-all-reduced over RCCL.
 
-Prints ONE JSON line on rank 0. ``value`` = gradient bytes processed by all ranks per
-second (GB/s). ``roofline`` = the final pass, the dominant kernel: k_final_odd (the last
-odd power iteration fused with the residual/output writes) or k_apply (residual + output
-after an even last iteration), timed with HIP events on the launch stream over the timed
-region.
-``cpu_baseline`` = the CPU oracle (bit-identical restatement of the reference) on a
-bounded sample, rank 0 at N = 1 only.
+N > 1: one process per GPU. Launched by the driver through ``torch.distributed.run`` (RANK /
+WORLD_SIZE / LOCAL_RANK in the environment), or, when started as ``python bench.py --gpus N``
+without them, this script starts ``torch.distributed.run`` itself as a child process BEFORE
+touching the GPU and exits with its code. Every rank holds its own gradients (data parallel,
+weak scaling) and the P/Q factors are SUM-all-reduced over RCCL. A rank count that differs from
+``--gpus`` is an error (exit 3).
+
+Cache state. The headline is COLD: the timed loop rotates over S (default 4) independent
+gradient sets, so between two uses of one set the other S-1 sets (gradients read and rewritten,
+fresh outputs written) stream > 256 MiB through the chip and the set is out of the 256 MiB
+Infinity Cache, as after a real backward pass. The same loop on ONE set (warm: the 102 MB
+ResNet-50 set plus its output fit the Infinity Cache) is reported beside it.
+
+Prints ONE JSON line on rank 0. ``value`` = gradient bytes processed by all ranks per second
+(GB/s, cold). ``roofline`` = the final pass, the dominant kernel: k_final_odd (the last odd
+power iteration fused with the residual/output writes) or k_apply, timed with HIP events that
+the library records on the launch stream around every such launch, over a second pass of the
+same cold rotation. ``cpu_baseline`` = the CPU oracle (bit-identical restatement of the
+reference) on a bounded sample, rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -22,6 +32,7 @@ import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
@@ -30,20 +41,24 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from powersgd_amd import Config, PowerSGD  # noqa: E402
-from powersgd_amd.workloads import CONFIGS  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
 def parse():
+    from powersgd_amd.workloads import CONFIGS
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2_resnet50_r1", choices=sorted(CONFIGS))
+    ap.add_argument("--sets", type=int, default=4, help="gradient sets rotated in the cold loop")
+    ap.add_argument("--mode", default="both", choices=["both", "cold", "warm"],
+                    help="profiling runs: time only one cache state (the headline needs 'both' or 'cold')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rendezvous + world-size report only (no codec; CPU-testable with gloo)")
     return ap.parse_args()
 
 
@@ -94,13 +109,15 @@ def step_alg_bytes(c, mask, world, fused):
     return total
 
 
-def load_pmc_traffic(cfg):
+def load_pmc_traffic(cfg, cache):
+    """HBM traffic per final-pass launch from the committed rocprofv3 --pmc passes."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(cfg)
+            d = json.load(f)
     except (OSError, ValueError):
         return None
+    return d.get(f"{cfg}:{cache}", d.get(cfg) if cache == "warm" else None)
 
 
 def cpu_baseline(c, seconds):
@@ -128,46 +145,27 @@ def cpu_baseline(c, seconds):
                       f"{t*1e3:.1f} ms, {sum(times):.1f} s total)"}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0
-        # over gloo exercises the N > 1 code path end to end; the real run is RCCL, one GPU
-        # per rank
-        if os.environ.get("PSGD_BENCH_ONE_DEVICE") == "1":
-            local = 0
-        torch.cuda.set_device(local)
-        backend = os.environ.get("PSGD_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            torch.distributed.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    c = dict(CONFIGS[a.config])
-    c["name"] = a.config
-    dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
-    shapes = c["shapes"]
+def launch_ranks(a) -> int:
+    """Start one rank per GPU with torch.distributed.run as a CHILD process (this process has
+    not touched the GPU: no exec from a GPU-initialised process) and return its exit code."""
+    import socket
 
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    grads = [torch.randn(s, generator=gen, device=dev, dtype=torch.float32).to(dtype) for s in shapes]
-    params = [torch.zeros(s, device=dev, dtype=dtype) for s in shapes]
-    psgd = PowerSGD(params, Config(c["rank"], c["mcr"], c["iters"], 0))
-    codec = psgd._powersgd
+    with socket.socket() as sk:  # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
-    for _ in range(a.warmup):
-        psgd.aggregate(grads)
-    torch.cuda.synchronize()
 
-    # timed region: K plain steps (no instrumentation inside)
+def timed(fn, steps, world, dev):
+    """Barrier + synchronize on both sides of `steps` calls; max wall time over ranks."""
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        psgd.aggregate(grads)
+    for k in range(steps):
+        fn(k)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -176,31 +174,114 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    # roofline pass: the same K steps again with HIP events around every final-pass launch,
-    # recorded by the library on the launch stream
-    codec._plan.set_timing(True)
-    for _ in range(a.steps):
-        psgd.aggregate(grads)
+    return elapsed
+
+
+def main():
+    a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.gpus > 1 and env_world is None:
+        sys.exit(launch_ranks(a))
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(3)
+    backend = os.environ.get("PSGD_BENCH_BACKEND", "nccl")
+    if a.launch_check:  # launcher + rendezvous only (CPU test with PSGD_BENCH_BACKEND=gloo)
+        if world > 1:
+            torch.distributed.init_process_group(backend)
+            world = torch.distributed.get_world_size()
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "backend": backend if world > 1 else None}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    from powersgd_amd import Config, PowerSGD
+    from powersgd_amd.workloads import CONFIGS
+
+    if world > 1:
+        # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0
+        # over gloo exercises the N > 1 code path end to end; the real run is RCCL, one GPU
+        # per rank
+        if os.environ.get("PSGD_BENCH_ONE_DEVICE") == "1":
+            local = 0
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
+        got = torch.distributed.get_world_size()
+        if got != a.gpus:
+            print(f"bench.py: process group reports {got} ranks, --gpus {a.gpus}", file=sys.stderr)
+            sys.exit(3)
+    dev = torch.device("cuda", local)
+    c = dict(CONFIGS[a.config])
+    c["name"] = a.config
+    dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+    shapes = c["shapes"]
+    S = max(1, a.sets)
+
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    sets = [[torch.randn(s, generator=gen, device=dev, dtype=torch.float32).to(dtype) for s in shapes]
+            for _ in range(S)]
+    params = [torch.zeros(s, device=dev, dtype=dtype) for s in shapes]
+    psgd = PowerSGD(params, Config(c["rank"], c["mcr"], c["iters"], 0))
+    codec = psgd._powersgd
+
+    for k in range(a.warmup):
+        psgd.aggregate(sets[k % S])
     torch.cuda.synchronize()
-    apply_total_ms, apply_launches = codec._plan.timing_read()
-    codec._plan.set_timing(False)
-    apply_ms = apply_total_ms / max(apply_launches, 1)
-    timed_first = codec.step_counter - a.steps  # step indices of the instrumented pass
+
+    # timed regions: K plain steps each (no instrumentation inside); cold = rotating sets
+    do_cold, do_warm = a.mode in ("both", "cold"), a.mode in ("both", "warm")
+    cold = timed(lambda k: psgd.aggregate(sets[k % S]), a.steps, world, dev) if do_cold else None
+    warm = timed(lambda k: psgd.aggregate(sets[0]), a.steps, world, dev) if do_warm else None
+
+    # roofline passes: the same K steps again with HIP events around every final-pass launch,
+    # recorded by the library on the launch stream
+    def kernel_pass(pick):
+        codec._plan.set_timing(True)
+        first = codec.step_counter
+        for k in range(a.steps):
+            psgd.aggregate(sets[pick(k)])
+        torch.cuda.synchronize()
+        total_ms, launches = codec._plan.timing_read()
+        codec._plan.set_timing(False)
+        return total_ms / max(launches, 1), first
+
+    apply_ms_cold, first_cold = kernel_pass(lambda k: k % S) if do_cold else (None, None)
+    apply_ms_warm, first_warm = kernel_pass(lambda k: 0) if do_warm else (None, None)
+    if first_cold is None:
+        first_cold = first_warm
 
     s = 2 if dtype == torch.bfloat16 else 4
     grad_bytes = sum(numel(x) for x in shapes) * s
-    ms_step = elapsed / a.steps * 1e3
-    value = world * grad_bytes * a.steps / elapsed / 1e9
     mask = psgd.is_compressed_mask
     # which final pass each timed step took (I odd: steps alternate between the fused last odd
     # iteration and k_apply); bytes are averaged over the timed steps
-    nf = sum(codec._plan.fused_final(t) for t in range(timed_first, codec.step_counter))
+    nf = sum(codec._plan.fused_final(t) for t in range(first_cold, first_cold + a.steps))
     frac_f = nf / a.steps
     ab = frac_f * apply_alg_bytes(c, mask, world, True) + (1 - frac_f) * apply_alg_bytes(c, mask, world, False)
     sb = frac_f * step_alg_bytes(c, mask, world, True) + (1 - frac_f) * step_alg_bytes(c, mask, world, False)
     kf = "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")")
     kname = kf if nf == a.steps else "k_apply (fused residual + output)" if nf == 0 else f"{kf} / k_apply, alternating"
-    achieved = ab / (apply_ms * 1e-3) / 1e9
+
+    def roof(apply_ms, cache):
+        ach = ab / (apply_ms * 1e-3) / 1e9
+        return {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(a.config, cache),
+                "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2), "cache": cache}
+
+    def step_roof(elapsed):
+        ms = elapsed / a.steps * 1e3
+        return {"alg_bytes_per_step": round(sb), "achieved_GBs": round(sb / (ms * 1e-3) / 1e9, 1),
+                "frac": round(sb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    head = cold if do_cold else warm
+    value = world * grad_bytes * a.steps / head / 1e9
     out = {
         "metric": "gradient GB/s compressed+decompressed (device-resident)",
         "value": round(value, 3),
@@ -208,24 +289,27 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(ms_step, 4),
+        "ms_per_step": round(head / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-        "data": "synthetic N(0,1) gradients of the named parameter shapes (torch.randn on device)",
+        "data": f"synthetic N(0,1) gradients of the named parameter shapes (torch.randn on device), "
+                (f"{S} independent sets rotated per step (cold Infinity Cache)" if do_cold else "one set (warm)"),
         "config": {"workload": a.config, "rank": c["rank"], "num_iters_per_step": c["iters"],
                    "min_compression_rate": c["mcr"], "tensors": len(shapes),
                    "compressed_tensors": sum(mask), "gradient_bytes_per_rank": grad_bytes,
-                   "parallelism": f"dp{world}"},
-        "roofline": {"kernel": kname, "bound": "hbm",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(a.config),
-                     "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2)},
-        "step_roofline": {"alg_bytes_per_step": round(sb),
-                          "achieved_GBs": round(sb / (ms_step * 1e-3) / 1e9, 1),
-                          "frac": round(sb / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                   "parallelism": f"dp{world}", "cache": "cold" if do_cold else "warm",
+                   "gradient_sets": S if do_cold else 1,
+                   "backend": (backend if world > 1 else None)},
+        "per_rank_GBs": round(value / world, 3),
+        "roofline": roof(apply_ms_cold, "cold") if do_cold else roof(apply_ms_warm, "warm"),
+        "step_roofline": step_roof(head),
     }
+    if do_cold and do_warm:
+        out["warm"] = {"value": round(world * grad_bytes * a.steps / warm / 1e9, 3),
+                       "ms_per_step": round(warm / a.steps * 1e3, 4),
+                       "roofline": roof(apply_ms_warm, "warm"), "step_roofline": step_roof(warm)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
     elif rank == 0:

@@ -19,6 +19,8 @@
 // collective, :204-219): writes the output, reads no gradient.
 #pragma once
 
+#include <atomic>
+
 #include "psgd_stream.cuh"
 
 namespace psgd {
@@ -584,11 +586,16 @@ hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, 
 template <typename T, int R, int SMAX, int K>
 hipError_t launch_final_lds_k(const FinalArgs& a, int ntiles, int lds_bytes, hipStream_t s, int* waves) {
     const void* fn = reinterpret_cast<const void*>(&k_final_lds<T, R, K, SMAX>);
-    static bool attr = false;  // opt in to > 64 KB of dynamic LDS once per instance
-    if (!attr) {
+    // opt in to > 64 KB of dynamic LDS once per instance AND device (the attribute is per
+    // device: a multi-device HostPowerSGD launches the same instance on several GPUs)
+    static std::atomic<uint64_t> attr_devs{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const uint64_t bit = uint64_t(1) << (dev & 63);
+    if (!(attr_devs.load() & bit)) {
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
         if (e != hipSuccess) return e;
-        attr = true;
+        attr_devs.fetch_or(bit);
     }
     if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
         int blocks = 0;

@@ -202,6 +202,96 @@ FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int sca
 
 int fin_bucket(int s) { return s <= 2 ? 2 : s <= 3 ? 3 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
 
+// Device-resident pointer tables (gradients, destinations) without a host synchronisation.
+// kSlots tables live in the caller's workspace; a call whose pointer set matches a slot uses
+// it as is (callers that rotate a few gradient sets, or get fresh tensors from the caching
+// allocator, hit after the first round). A miss takes the least recently used slot and
+// uploads into it with hipMemcpyAsync ON THE LAUNCH STREAM from a pinned staging copy, so
+// the copy is ordered after every earlier launch on that stream that may still read the
+// slot, and the host never waits (the reference hands tensors to torch ops, which never
+// synchronise either). Calls of one plan must be ordered on one stream (as torch's are).
+struct TableCache {
+    static constexpr int kSlots = 4;
+    size_t n = 0;              // pointers per table
+    char* dev = nullptr;       // kSlots * n pointers inside the workspace
+    std::vector<void*> host[kSlots];
+    uint64_t stamp[kSlots] = {};
+    uint64_t clock = 0;
+    int cur = -1;
+    void** pinned = nullptr;   // kSlots * n staging pointers (hipHostMalloc)
+    hipEvent_t ev[kSlots] = {};
+    bool live[kSlots] = {};
+
+    static size_t bytes(size_t n) { return size_t(kSlots) * std::max<size_t>(n, 1) * sizeof(void*); }
+    void bind(char* d, size_t count) {
+        release();
+        dev = d;
+        n = count;
+        for (auto& h : host) h.clear();
+        cur = -1;
+    }
+    void release() {
+        for (int i = 0; i < kSlots; ++i) {
+            if (live[i]) (void)hipEventSynchronize(ev[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            ev[i] = nullptr;
+            live[i] = false;
+        }
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+    }
+    ~TableCache() { release(); }
+    bool match(int i, void* const* p) const {
+        if (host[i].size() != n) return false;
+        for (size_t k = 0; k < n; ++k)
+            if (host[i][k] != p[k]) return false;
+        return true;
+    }
+    // 0 on success, else a hipError_t
+    hipError_t select(void* const* p, hipStream_t s) {
+        ++clock;
+        if (cur >= 0 && match(cur, p)) {
+            stamp[cur] = clock;
+            return hipSuccess;
+        }
+        int victim = 0;
+        for (int i = 0; i < kSlots; ++i) {
+            if (match(i, p)) {
+                cur = i;
+                stamp[i] = clock;
+                return hipSuccess;
+            }
+            if (stamp[i] < stamp[victim]) victim = i;
+        }
+        if (!pinned) {
+            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&pinned), bytes(n), hipHostMallocDefault);
+            if (e != hipSuccess) {
+                pinned = nullptr;
+                return e;
+            }
+            for (int i = 0; i < kSlots; ++i)
+                if ((e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+        }
+        // the staging slot may still feed the previous upload into this slot
+        if (live[victim]) {
+            const hipError_t e = hipEventSynchronize(ev[victim]);
+            if (e != hipSuccess) return e;
+        }
+        void** stage = pinned + size_t(victim) * n;
+        std::copy(p, p + n, stage);
+        hipError_t e = hipMemcpyAsync(dev + size_t(victim) * n * sizeof(void*), stage, n * sizeof(void*),
+                                      hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipEventRecord(ev[victim], s);
+        if (e != hipSuccess) return e;
+        live[victim] = true;
+        host[victim].assign(p, p + n);
+        stamp[victim] = clock;
+        cur = victim;
+        return hipSuccess;
+    }
+    void* const* table() const { return reinterpret_cast<void* const*>(dev + size_t(cur) * n * sizeof(void*)); }
+};
+
 struct DevScope {  // make `dev` current for the scope, restore afterwards
     int prev = -1;
     explicit DevScope(int dev) {
@@ -249,7 +339,7 @@ struct psgd_plan {
     std::vector<OrthUnit> units_p, units_q;
     std::vector<OrthUnit> munits_p, munits_q;  // one unit per MATRIX (paper-code Gram-Schmidt)
     size_t o_munits_p = 0, o_munits_q = 0, o_rdst = 0, o_odst = 0;
-    std::vector<void*> host_rdst, host_odst;
+    TableCache grad_tab, rdst_tab, odst_tab;  // device pointer tables (gradients, destinations)
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_floats = 0;
     double unc_floats = 0, comp_floats = 0;
@@ -266,7 +356,6 @@ struct psgd_plan {
     float* P = nullptr;
     float* Q = nullptr;
     char* ws = nullptr;
-    std::vector<void*> host_ptrs;
     void* out_now = nullptr;  // psgd_aggregate's output buffer (fused final pass)
     // benchmark timing of k_apply: event pairs recorded on the launch stream
     bool timing = false;
@@ -428,7 +517,7 @@ struct psgd_flat {
     bool bound = false;
     int device = -1;
     char* ws = nullptr;
-    std::vector<void*> host_ptrs;
+    TableCache tab;  // device pointer tables of the tensors
 };
 
 namespace {
@@ -439,26 +528,27 @@ int upload(void* dst, const void* src, size_t bytes) {
     return PSGD_OK;
 }
 
-// Upload the gradient pointer table when it changed; switch matrices whose gradient is not
-// vector-aligned to the scalar path (rare: views into unaligned flat buffers).
+// Select (or upload, stream-ordered) the gradient pointer table; switch matrices whose
+// gradient is not vector-aligned to the scalar path (rare: views into unaligned flat buffers;
+// only that re-tiling synchronises, because the tile tables are rewritten in place).
 int refresh_pointers(psgd_plan* p, void* const* grads, hipStream_t stream) {
     const size_t nt = p->shapes.size();
-    bool same = p->host_ptrs.size() == nt;
-    for (size_t i = 0; same && i < nt; ++i) same = p->host_ptrs[i] == grads[i];
-    if (same) return PSGD_OK;
     for (size_t i = 0; i < nt; ++i)
         if (!grads[i]) return fail(PSGD_ERR_VALUE, "null gradient pointer");
-    std::vector<int> vec(p->mats.size());
     const uintptr_t need = p->dtype == PSGD_F32 ? 16 : 8;
-    for (size_t i = 0; i < p->mats.size(); ++i)
-        vec[i] = p->base_vec[i] && (reinterpret_cast<uintptr_t>(grads[p->mats[i].tensor]) % need == 0);
-    PSGD_HIP(hipStreamSynchronize(stream));  // earlier launches may still read the tables
-    if (vec != p->vec_now) {
+    bool same_vec = true;
+    for (size_t i = 0; same_vec && i < p->mats.size(); ++i)
+        same_vec = p->vec_now[i] == int(p->base_vec[i] && (reinterpret_cast<uintptr_t>(grads[p->mats[i].tensor]) % need == 0));
+    if (!same_vec) {
+        std::vector<int> vec(p->mats.size());
+        for (size_t i = 0; i < p->mats.size(); ++i)
+            vec[i] = p->base_vec[i] && (reinterpret_cast<uintptr_t>(grads[p->mats[i].tensor]) % need == 0);
+        PSGD_HIP(hipStreamSynchronize(stream));  // earlier launches may still read the tile tables
         p->set_vec(vec);
         if (int st = p->upload_tiles()) return st;
     }
-    p->host_ptrs.assign(grads, grads + nt);
-    return upload(p->dev<void>(p->o_ptrs), p->host_ptrs.data(), nt * sizeof(void*));
+    PSGD_HIP(p->grad_tab.select(grads, stream));
+    return PSGD_OK;
 }
 
 }  // namespace
@@ -680,7 +770,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         off = align256(off + bytes);
         return o;
     };
-    p->o_ptrs = carve(size_t(num_tensors) * sizeof(void*));
+    p->o_ptrs = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_mats = carve(p->mats.size() * sizeof(MatDesc));
     p->o_tiles = carve(size_t(p->tiles_cap) * sizeof(Tile));
     p->o_tiles_ov = carve(size_t(p->tiles_cap) * sizeof(Tile));
@@ -696,8 +786,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     }
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
-    p->o_rdst = carve(size_t(num_tensors) * sizeof(void*));
-    p->o_odst = carve(size_t(num_tensors) * sizeof(void*));
+    p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
+    p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
     p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
     p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
@@ -774,15 +864,16 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     p->P = P;
     p->Q = Q;
     p->ws = static_cast<char*>(workspace);
-    p->host_ptrs.clear();
+    const size_t nt = p->shapes.size();
+    p->grad_tab.bind(p->dev<char>(p->o_ptrs), nt);
+    p->rdst_tab.bind(p->dev<char>(p->o_rdst), nt);
+    p->odst_tab.bind(p->dev<char>(p->o_odst), nt);
     if (int st = p->upload_tiles()) return st;
     if (int st = upload(p->dev<void>(p->o_red_even), p->red_even.data(), p->red_even.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_munits_p), p->munits_p.data(), p->munits_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_munits_q), p->munits_q.data(), p->munits_q.size() * sizeof(OrthUnit))) return st;
-    p->host_rdst.clear();
-    p->host_odst.clear();
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
@@ -857,7 +948,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         FinalArgs fa{};
         fa.mats = p->dev<MatDesc>(p->o_mats);
         fa.tiles = p->dev<Tile>(p->o_tiles_fin);
-        fa.grads = p->dev<void* const>(p->o_ptrs);
+        fa.grads = p->grad_tab.table();
         fa.out = p->out_now;
         fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
         fill_terms(p, step, it, fa.res);
@@ -888,7 +979,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
     pa.tiles = p->dev<Tile>(p->o_tiles);
-    pa.grads = p->dev<void* const>(p->o_ptrs);
+    pa.grads = p->grad_tab.table();
     pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
     if (fused0) {
@@ -956,7 +1047,7 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     ApplyArgs aa{};
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles);
-    aa.grads = p->dev<void* const>(p->o_ptrs);
+    aa.grads = p->grad_tab.table();
     aa.out = out;
     fill_terms(p, step, I, aa.res);
     float* last = p->even(step, I - 1) ? p->Q : p->P;  // all-reduced factor of the last iteration
@@ -1013,7 +1104,7 @@ int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, 
     if (int st = refresh_pointers(p, grads, s)) return st;
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
-    pa.grads = p->dev<void* const>(p->o_ptrs);
+    pa.grads = p->grad_tab.table();
     pa.x = x;
     pa.part = p->dev<float>(p->o_part);
     for (int k = 0; k < nterms; ++k) {
@@ -1066,22 +1157,17 @@ int psgd_orthogonalize(psgd_plan* p, int32_t which, float* buf, int32_t mode, vo
     return PSGD_OK;
 }
 
-// upload a per-tensor destination table when it changed; every pointer must keep the
-// vector layout's alignment where the matrix uses it
-static int refresh_table(psgd_plan* p, void* const* ptrs, std::vector<void*>& host, size_t off, hipStream_t s) {
-    const size_t nt = p->shapes.size();
+// select (or upload, stream-ordered) a per-tensor destination table; every pointer must keep
+// the vector layout's alignment where the matrix uses it
+static int refresh_table(psgd_plan* p, void* const* ptrs, TableCache& tab, hipStream_t s) {
     const uintptr_t need = p->dtype == PSGD_F32 ? 16 : 8;
     for (const MatDesc& md : p->mats) {
         if (!ptrs[md.tensor]) return fail(PSGD_ERR_VALUE, "null destination pointer");
         if (md.vec && reinterpret_cast<uintptr_t>(ptrs[md.tensor]) % need)
             return fail(PSGD_ERR_LAYOUT, "destination tensor is not aligned for the vector layout");
     }
-    bool same = host.size() == nt;
-    for (size_t i = 0; same && i < nt; ++i) same = host[i] == ptrs[i];
-    if (same) return PSGD_OK;
-    PSGD_HIP(hipStreamSynchronize(s));
-    host.assign(ptrs, ptrs + nt);
-    return upload(p->dev<void>(off), host.data(), nt * sizeof(void*));
+    PSGD_HIP(tab.select(ptrs, s));
+    return PSGD_OK;
 }
 
 int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, void* const* out, int32_t nterms,
@@ -1096,14 +1182,14 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int st = refresh_pointers(p, grads, s)) return st;
     if (resid_out)
-        if (int st = refresh_table(p, resid_out, p->host_rdst, p->o_rdst, s)) return st;
-    if (int st = refresh_table(p, out, p->host_odst, p->o_odst, s)) return st;
+        if (int st = refresh_table(p, resid_out, p->rdst_tab, s)) return st;
+    if (int st = refresh_table(p, out, p->odst_tab, s)) return st;
     ApplyArgs aa{};
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles);
-    aa.grads = p->dev<void* const>(p->o_ptrs);
-    aa.rdst = resid_out ? p->dev<void* const>(p->o_rdst) : nullptr;
-    aa.odst = p->dev<void* const>(p->o_odst);
+    aa.grads = p->grad_tab.table();
+    aa.rdst = resid_out ? p->rdst_tab.table() : nullptr;
+    aa.odst = p->odst_tab.table();
     bool shared = alpha == 1.0f;
     for (int k = 0; k < nterms; ++k) {
         aa.res.p[k] = term_p[k];
@@ -1189,7 +1275,7 @@ int psgd_flat_create(const int64_t* numels, int32_t count, int32_t dtype, psgd_f
     for (size_t e = 0; e < f->entries.size(); ++e)
         for (int64_t st = 0; st < f->entries[e].numel; st += kFlatItem) f->items.push_back(FlatItem{int32_t(e), 0, st});
     f->o_ptrs = 0;
-    f->o_ents = align256(size_t(std::max(count, 1)) * sizeof(void*));
+    f->o_ents = align256(TableCache::bytes(size_t(std::max(count, 1))));
     f->o_items = align256(f->o_ents + std::max<size_t>(f->entries.size(), 1) * sizeof(FlatEntry));
     f->ws_bytes = align256(f->o_items + std::max<size_t>(f->items.size(), 1) * sizeof(FlatItem));
     *out = f;
@@ -1212,29 +1298,22 @@ int psgd_flat_bind(psgd_flat* f, int32_t device, void* workspace) {
     DevScope scope(device);
     f->device = device;
     f->ws = static_cast<char*>(workspace);
-    f->host_ptrs.clear();
+    f->tab.bind(f->ws + f->o_ptrs, size_t(f->count));
     if (int st = upload(f->ws + f->o_ents, f->entries.data(), f->entries.size() * sizeof(FlatEntry))) return st;
     if (int st = upload(f->ws + f->o_items, f->items.data(), f->items.size() * sizeof(FlatItem))) return st;
     f->bound = true;
     return PSGD_OK;
 }
 
-// Device-side arguments of a flat pack (uploads the pointer table when it changed).
+// Device-side arguments of a flat pack (selects or uploads the pointer table, stream-ordered).
 static int flat_args(psgd_flat* f, void* const* tensors, void* flat, int32_t world, hipStream_t s,
                      FlatArgs* out) {
-    const size_t n = size_t(f->count);
-    bool same = f->host_ptrs.size() == n;
-    for (size_t i = 0; same && i < n; ++i) same = f->host_ptrs[i] == tensors[i];
-    if (!same) {
-        PSGD_HIP(hipStreamSynchronize(s));
-        f->host_ptrs.assign(tensors, tensors + n);
-        if (int st = upload(f->ws + f->o_ptrs, f->host_ptrs.data(), n * sizeof(void*))) return st;
-    }
+    PSGD_HIP(f->tab.select(tensors, s));
     FlatArgs& a = *out;
     a = FlatArgs{};
     a.entries = reinterpret_cast<const FlatEntry*>(f->ws + f->o_ents);
     a.items = reinterpret_cast<const FlatItem*>(f->ws + f->o_items);
-    a.tensors = reinterpret_cast<void* const*>(f->ws + f->o_ptrs);
+    a.tensors = f->tab.table();
     a.flat = flat;
     a.nitems = int32_t(f->items.size());
     a.world = world;

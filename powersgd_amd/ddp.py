@@ -1,29 +1,34 @@
 """DistributedDataParallel communication hook running this package's PowerSGD codec.
 
 The reference drives PowerSGD from the optimizer (``optimizer_step``, powersgd/__init__.py:
-7-25) and keeps the error-feedback residual in ``p.grad``, so the next backward adds onto it.
-Under ``DistributedDataParallel`` the gradients reach the aggregator as buckets through
-``register_comm_hook`` (the paper code compares against the upstream hook that way,
-SURVEY.md §8(f) row 3). This adapter keeps the reference's algorithm and semantics per bucket:
+7-25): ONE ``PowerSGD`` over all parameters in optimizer order, the error-feedback residual
+kept in ``p.grad`` so the next backward adds onto it (README.md:39-42). Under
+``DistributedDataParallel`` the gradients reach the aggregator bucket by bucket through
+``register_comm_hook`` (the paper code plugs PowerSGD in that way, paper-code/
+train_pytorch.py:106-131). This adapter reproduces the reference flow exactly, independent of
+how DDP buckets the parameters (and of its bucket rebuild after the first iteration):
 
-* one ``PowerSGD`` per bucket layout (shapes + dtype), i.e. the same warm-up, compression mask,
-  shape-group batching, P/Q state and step counter as the reference applied to that bucket's
-  gradients (reference :41-105, :113-275);
-* error feedback exactly as the reference gets it through autograd accumulation: the stored
-  residual is added to the fresh bucket gradients before the codec runs (README.md:39-42),
-  and the codec leaves the new residual in that buffer;
-* the averaged approximation (plus the uncompressed averages) is returned to DDP, which
-  writes it into ``p.grad`` for the optimizer.
+* the state owns one ``PowerSGD`` over ``params`` in the given (optimizer) order — the same
+  compression mask, shape-group batching, P/Q state and step counter as the reference's
+  ``PowerSGD(params, config)`` (reference :41-105, :113-275);
+* it owns the error-feedback residual per parameter (one flat buffer): each bucket's fresh
+  gradients are ADDED to their parameters' residual (what autograd's accumulation into
+  ``p.grad`` does in the reference flow);
+* a bucket's future completes when the LAST bucket of the iteration has arrived: then one
+  ``aggregate`` runs over all parameters (its factor all-reduces on the default process group,
+  reference :207) and every pending bucket receives its averaged approximation in its own
+  layout. DDP waits on all bucket futures only after backward has launched every hook, so the
+  deferral is legal; it trades DDP's per-bucket overlap for the reference's exact semantics.
 
-The factor all-reduces use the default process group, like the reference (:207).
+Because the residual lives in the state (not in ``p.grad``), the training loop zeroes
+gradients as usual:
 
-    from powersgd_amd import Config
-    from powersgd_amd.ddp import PowerSGDState, powersgd_hook
-    ddp_model.register_comm_hook(PowerSGDState(Config(rank=1, num_iters_per_step=2,
-                                                      start_compressing_after_num_steps=0)),
-                                 powersgd_hook)
+    state = PowerSGDState(Config(rank=2, num_iters_per_step=2, start_compressing_after_num_steps=0),
+                          params=[p for p in model.parameters()])
+    ddp_model.register_comm_hook(state, powersgd_hook)
+    loss.backward(); optimizer.step(); optimizer.zero_grad()
 """
-from typing import Dict, Tuple
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -32,53 +37,61 @@ from .powersgd import Config, PowerSGD
 
 
 class PowerSGDState:
-    """Hook state: one codec + residual (error-feedback) buffer per SET of bucket parameters.
+    """Hook state: one codec + residual buffer over ``params`` (the optimizer's order)."""
 
-    Keyed by the parameters rather than the bucket layout: DDP rebuilds its buckets after the
-    first iteration (new order inside a bucket), and the residual and P/Q state must follow
-    the parameters through that. The codec batches the parameters in the order the set was
-    first seen."""
-
-    def __init__(self, config: Config, process_group=None):
+    def __init__(self, config: Config, params, process_group=None):
         if process_group is not None and process_group is not dist.group.WORLD:
             raise ValueError("powersgd_hook all-reduces on the default process group (reference :207)")
         self.config = config
-        self._sets: Dict[frozenset, dict] = {}
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise IndexError("list index out of range")  # the reference's PowerSGD on []
+        self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        numel = sum(p.numel() for p in self.params)
+        p0 = self.params[0]
+        self.residual = torch.zeros(numel, dtype=p0.dtype, device=p0.device)
+        self.views: List[torch.Tensor] = []
+        off = 0
+        for p in self.params:
+            self.views.append(self.residual[off:off + p.numel()].view(p.shape))
+            off += p.numel()
+        self.powersgd = PowerSGD(self.views, config)
+        self._seen = [False] * len(self.params)
+        self._nseen = 0
+        self._pending: List[tuple] = []
 
-    def _entry(self, params) -> dict:
-        key = frozenset(id(p) for p in params)
-        e = self._sets.get(key)
-        if e is None:
-            numel = sum(p.numel() for p in params)
-            resid = torch.zeros(numel, dtype=params[0].dtype, device=params[0].device)
-            views, off = [], 0
-            for p in params:
-                views.append(resid[off:off + p.numel()].view(p.shape))
-                off += p.numel()
-            e = {"ids": [id(p) for p in params], "resid": resid, "views": views,
-                 "psgd": PowerSGD(views, self.config)}
-            self._sets[key] = e
-        return e
+    def _arrive(self, bucket: "dist.GradBucket") -> "torch.futures.Future[torch.Tensor]":
+        params, grads = bucket.parameters(), bucket.gradients()
+        idx = []
+        for p, g in zip(params, grads):
+            i = self._index.get(id(p))
+            if i is None:
+                raise RuntimeError("DDP bucket holds a parameter that PowerSGDState was not given")
+            if self._seen[i]:
+                raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
+            self.views[i].add_(g)  # error feedback: residual + fresh gradient
+            self._seen[i] = True
+            self._nseen += 1
+            idx.append(i)
+        fut: torch.futures.Future = torch.futures.Future()
+        self._pending.append((bucket.buffer(), grads, idx, fut))
+        if self._nseen == len(self.params):
+            self._complete()
+        return fut
+
+    def _complete(self) -> None:
+        outs = self.powersgd.aggregate(self.views)  # leaves the new residual in self.views
+        pending, self._pending = self._pending, []
+        self._seen = [False] * len(self.params)
+        self._nseen = 0
+        for buf, grads, idx, fut in pending:
+            out = torch.empty_like(buf)
+            for g, i in zip(grads, idx):
+                off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
+                out[off:off + g.numel()].view(g.shape).copy_(outs[i])
+            fut.set_result(out)
 
 
-def powersgd_hook(state: PowerSGDState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
-    """``DistributedDataParallel.register_comm_hook`` hook: PowerSGD on one gradient bucket."""
-    params = bucket.parameters()
-    grads = bucket.gradients()
-    e = state._entry(params)
-    slot = {id(p): g for p, g in zip(params, grads)}
-    # error feedback: residual += fresh gradients (what autograd accumulation does to the
-    # reference's p.grad); the codec then leaves the new residual in the same buffer
-    for pid, r in zip(e["ids"], e["views"]):
-        r.add_(slot[pid])
-    outs = e["psgd"].aggregate(e["views"])
-    # the averaged gradients go back in the bucket's own layout
-    buf = bucket.buffer()
-    out = torch.empty_like(buf)
-    for pid, o in zip(e["ids"], outs):
-        g = slot[pid]
-        off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
-        out[off:off + g.numel()].view(g.shape).copy_(o)
-    fut: torch.futures.Future[torch.Tensor] = torch.futures.Future()
-    fut.set_result(out)
-    return fut
+def powersgd_hook(state: PowerSGDState, bucket: "dist.GradBucket") -> "torch.futures.Future[torch.Tensor]":
+    """``DistributedDataParallel.register_comm_hook`` hook: the reference's PowerSGD flow."""
+    return state._arrive(bucket)

@@ -27,13 +27,13 @@ the codec on the GPUs:
 """
 from __future__ import annotations
 
-import sys
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from .powersgd import BasicConfig, BasicPowerSGD, Config, avg_compressed_size
+from .utils import is_distributed
 
 
 class HostPowerSGD:
@@ -42,6 +42,11 @@ class HostPowerSGD:
     def __init__(self, params: List[torch.Tensor], config: Config, devices: Optional[Sequence[int]] = None,
                  chunks: int = 2):
         params = list(params)
+        if is_distributed():
+            # world-size-1 semantics only: the factors of every bin would be all-reduced while
+            # the uncompressed and warm-up paths stay local (a mix of global and local means)
+            raise RuntimeError("HostPowerSGD serves one process (world size 1); with a process group "
+                               "use PowerSGD on GPU-resident gradients, one rank per GPU")
         self.config = config
         self.device = params[0].device  # as the reference: the parameters' device (CPU here)
         if self.device.type != "cpu":
@@ -102,7 +107,6 @@ class HostPowerSGD:
             off += self.shapes[i].numel()
         self.numel = off
         self.host_grads = torch.zeros(self.numel, dtype=self.dtype).pin_memory()
-        self._new_outputs()
 
         # per bin: device buffer, codec, streams; the codec's state comes from the host init
         self.streams: Dict[int, tuple] = {}
@@ -121,14 +125,11 @@ class HostPowerSGD:
                 bn["events"] = [torch.cuda.Event(), torch.cuda.Event()]
 
     def _new_outputs(self) -> None:
-        self.host_out = torch.empty(self.numel, dtype=self.dtype).pin_memory()
+        """Fresh pinned outputs every step, as the reference returns fresh tensors (a caller
+        may hold last step's outputs). torch's caching host allocator recycles the block of
+        an output nobody holds any more once its copies have completed."""
+        self.host_out = torch.empty(self.numel, dtype=self.dtype, pin_memory=True)
         self._out_views = [self._view(self.host_out, i) for i in range(len(self.shapes))]
-        self._out_refs = [sys.getrefcount(v) for v in self._out_views]
-
-    def _outputs_free(self) -> bool:
-        """No reference to last step's outputs survives (the reference returns fresh
-        tensors every step, so a held output must not be overwritten)."""
-        return [sys.getrefcount(v) for v in self._out_views] == self._out_refs
 
     def _view(self, flat: torch.Tensor, i: int, base: int = 0) -> torch.Tensor:
         o = self.offsets[i] - base
@@ -156,14 +157,15 @@ class HostPowerSGD:
         for g, s in zip(gradients, self.shapes):
             if g.shape != s or g.dtype != self.dtype or g.device.type != "cpu":
                 raise RuntimeError("gradients must match the parameters' shapes, dtype and device")
+        if is_distributed():
+            raise RuntimeError("HostPowerSGD serves one process (world size 1)")
         self.step_counter += 1
         if self.step_counter <= self.config.start_compressing_after_num_steps:
             outs = [g.clone() for g in gradients]  # AllReduce at world size 1: copy, zero
             for g in gradients:
                 g.zero_()
             return outs
-        if not self._outputs_free():
-            self._new_outputs()
+        self._new_outputs()
         direct = self._pinned_in_place(gradients)
         if not direct:
             for i, g in enumerate(gradients):

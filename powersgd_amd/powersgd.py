@@ -14,16 +14,14 @@ Differences, all deliberate:
 * Device tensors on a ROCm GPU only; the HIP library is mandatory (no CPU fallback).
 * bfloat16 gradients are supported (the reference raises at its ``bmm``, :189): the
   gradient matrix is read/written in bf16, factors and arithmetic stay fp32.
-* Returned compressed outputs are views of one flat buffer instead of separate
-  ``empty_like`` tensors (uncompressed outputs are views in the reference too). The
-  buffer is reused across steps only when its storage proves nobody else holds a
-  reference to it, so the reuse is not observable.
+* Returned compressed outputs are views of one flat buffer (allocated fresh per call)
+  instead of separate ``empty_like`` tensors; uncompressed outputs are views in the
+  reference too.
 """
 from __future__ import annotations
 
 import ctypes
 import os
-import sys
 from abc import ABC, abstractmethod
 from collections import defaultdict
 from typing import Dict, List, NamedTuple, Optional, Sequence, Union
@@ -64,35 +62,18 @@ def _stream(device: torch.device) -> int:
 
 
 class _OutputSlab:
-    """Flat output buffer + views, reused only while nothing outside holds them.
-
-    "Nothing holds them" = no Python reference to any returned view survives (refcounts
-    back to the cached baseline) AND no other tensor shares the storage (storage use
-    count back to baseline). Otherwise a fresh buffer is allocated, exactly like the
-    reference's per-call ``empty_like``.
-    """
+    """A FRESH flat output buffer + views per call, like the reference's per-call
+    ``empty_like`` (:153): a caller may keep last step's outputs (``p.grad = out``, tensors
+    saved by autograd) and they are never overwritten. The caching allocator hands back the
+    block of an output nobody holds any more, so this costs no device allocation in steady
+    state. ``flat`` is the buffer of the latest call."""
 
     def __init__(self):
         self.flat: Optional[torch.Tensor] = None
-        self.views: List[torch.Tensor] = []
-        self._base_uses = 0
-        self._base_refs: List[int] = []
-
-    def _uses(self) -> int:
-        return torch._C._storage_Use_Count(self.flat.untyped_storage()._cdata)
-
-    def _refs(self) -> List[int]:
-        return [sys.getrefcount(v) for v in self.views]
 
     def get(self, numel: int, shapes: Sequence[torch.Size], dtype, device) -> List[torch.Tensor]:
-        if self.flat is not None and self._uses() == self._base_uses and self._refs() == self._base_refs:
-            return list(self.views)
-        flat = torch.empty(max(numel, 1), dtype=dtype, device=device)
-        self.views = _views(flat, shapes)
-        self.flat = flat
-        self._base_uses = self._uses()
-        self._base_refs = self._refs()
-        return list(self.views)
+        self.flat = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        return _views(self.flat, shapes)
 
 
 class Aggregator(ABC):

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 from golden_io import load, manifest, scenario_inputs
+from parity_log import check
 
 pytestmark = pytest.mark.gpu
 MAN = manifest()
@@ -42,7 +43,8 @@ def _worker(rank_id, world, key, initfile):
                 scale = max(float(g.norm()), 1e-30)
                 eo = float((outs[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_out_{i}"])).norm()) / scale
                 er = float((grads[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_res_{i}"])).norm()) / scale
-                assert eo <= TOL_FREE and er <= TOL_FREE, (key, rank_id, t, i, eo, er)
+                check(eo, TOL_FREE, key, rank_id, t, i, "out")
+                check(er, TOL_FREE, key, rank_id, t, i, "res")
             res = [g.cpu() for g in grads]
         torch.distributed.barrier()
     finally:

@@ -20,6 +20,7 @@ import pytest
 import torch
 
 from golden_io import checksums, config_grads, config_state0, load, manifest, scenario_inputs
+from parity_log import check
 from oracle import powersgd_oracle as O
 from powersgd_amd import Config, PowerSGD
 from powersgd_amd.workloads import CONFIGS, hash_tensors, resnet50_shapes
@@ -73,8 +74,8 @@ def test_golden_per_step(name):
         for i, g in enumerate(inputs):
             wo = torch.from_numpy(want[f"s{t}_out_{i}"])
             wr = torch.from_numpy(want[f"s{t}_res_{i}"])
-            assert _rel(outs[i], wo, g) <= TOL_STEP, (name, t, i, "out", _rel(outs[i], wo, g))
-            assert _rel(grads[i], wr, g) <= TOL_STEP, (name, t, i, "res", _rel(grads[i], wr, g))
+            check(_rel(outs[i], wo, g), TOL_STEP, name, t, i, "out")
+            check(_rel(grads[i], wr, g), TOL_STEP, name, t, i, "res")
         assert [psgd.step_counter, psgd._powersgd.step_counter] == list(want[f"s{t}_step"])
         res_ref = [torch.from_numpy(want[f"s{t}_res_{i}"]) for i in range(len(shapes))]
 
@@ -95,8 +96,8 @@ def test_golden_free_running(name):
         for i, g in enumerate(inputs):
             wo = torch.from_numpy(want[f"s{t}_out_{i}"])
             wr = torch.from_numpy(want[f"s{t}_res_{i}"])
-            assert _rel(outs[i], wo, g) <= TOL_FREE, (name, t, i, "out", _rel(outs[i], wo, g))
-            assert _rel(grads[i], wr, g) <= TOL_FREE, (name, t, i, "res", _rel(grads[i], wr, g))
+            check(_rel(outs[i], wo, g), TOL_FREE, name, t, i, "out")
+            check(_rel(grads[i], wr, g), TOL_FREE, name, t, i, "res")
         res = [x.cpu() for x in grads]
 
 
@@ -166,16 +167,16 @@ def test_baseline_configs_vs_oracle(cfg):
     for t, inputs, og, oc, rg, rc in _oracle_and_gpu(cfg, steps):
         tol = TOL_STEP * 4 if t == 0 else TOL_FREE
         for i, g in enumerate(inputs):
-            assert _rel(og[i], oc[i], g) <= tol, (cfg, t, i, "out", _rel(og[i], oc[i], g))
-            assert _rel(rg[i], rc[i], g) <= tol, (cfg, t, i, "res", _rel(rg[i], rc[i], g))
+            check(_rel(og[i], oc[i], g), tol, cfg, t, i, "out")
+            check(_rel(rg[i], rc[i], g), tol, cfg, t, i, "res")
 
 
 @pytest.mark.slow
 def test_baseline_bf16_llama_vs_oracle():
     for t, inputs, og, oc, rg, rc in _oracle_and_gpu("cfg4_llama_r2_bf16", 1, torch.bfloat16):
         for i, g in enumerate(inputs):
-            assert _rel(og[i], oc[i], g) <= TOL_BF16, ("out", i, _rel(og[i], oc[i], g))
-            assert _rel(rg[i], rc[i], g) <= TOL_BF16, ("res", i, _rel(rg[i], rc[i], g))
+            check(_rel(og[i], oc[i], g), TOL_BF16, "cfg4", i, "out")
+            check(_rel(rg[i], rc[i], g), TOL_BF16, "cfg4", i, "res")
 
 
 @pytest.mark.slow
@@ -191,7 +192,7 @@ def test_resnet50_error_feedback_identity_and_determinism(rank, iters):
         outs = psgd.aggregate(grads)
         torch.cuda.synchronize()
         for o, a, r in zip(orig, outs, grads):
-            assert _rel(a + r, o, o) <= 1e-6
+            check(_rel(a + r, o, o), 1e-6, rank, iters, "ef-identity")
         runs.append(([a.clone() for a in outs], [g.clone() for g in grads],
                      psgd._powersgd._ps_buffer.clone(), psgd._powersgd._qs_buffer.clone()))
     for x, y in zip(runs[0][0] + runs[0][1], runs[1][0] + runs[1][1]):
@@ -217,7 +218,7 @@ def test_orthonormal_in_factor_every_rank_bucket(rank):
     ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())  # Q is overwritten anyway at it 0
     oc = O.policy_step(ora, [g.cpu() for g in orig])
     for i, g in enumerate(orig):
-        assert _rel(outs[i], oc[i], g) <= TOL_STEP, (rank, i, _rel(outs[i], oc[i], g))
+        check(_rel(outs[i], oc[i], g), TOL_STEP, rank, i, "out")
 
 
 @pytest.mark.parametrize("rank,iters", [(12, 2), (16, 2), (16, 3), (32, 2)])
@@ -242,6 +243,6 @@ def test_wide_rank_free_running(rank, iters):
         oc = O.policy_step(ora, gc)
         torch.cuda.synchronize()
         for i, g in enumerate(scale):
-            assert _rel(od[i], oc[i], g) <= TOL_FREE, (t, i, "out", _rel(od[i], oc[i], g))
-            assert _rel(gd[i], gc[i], g) <= TOL_FREE, (t, i, "res", _rel(gd[i], gc[i], g))
+            check(_rel(od[i], oc[i], g), TOL_FREE, rank, iters, t, i, "out")
+            check(_rel(gd[i], gc[i], g), TOL_FREE, rank, iters, t, i, "res")
         res_d, res_c = gd, gc

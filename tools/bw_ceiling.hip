@@ -302,6 +302,45 @@ int main() {
         }, 50);
         printf("read+r1w2 grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 4 * bytes / t / 1e3);
     }
+    // COLD ceilings: 4 independent (G, out) pairs of the same size rotated per launch, so
+    // between two uses of a pair ~600 MB stream through the chip (> the 256 MiB Infinity
+    // Cache): the rate a step gets when the gradients arrive cold from a backward pass
+    {
+        constexpr int NS = 4;
+        v4f *gs[NS], *os[NS];
+        for (int i = 0; i < NS; ++i) {
+            CK(hipMalloc(&gs[i], bytes));
+            CK(hipMalloc(&os[i], bytes));
+            CK(hipMemset(gs[i], 0, bytes));
+            CK(hipMemset(os[i], 0, bytes));
+        }
+        int k = 0;
+        for (int gr : {4096, 8192, 16384}) {
+            float t;
+            t = time_it([&] { k_read<8><<<gr, 256>>>(gs[k % NS], sink, n4); ++k; }, 40);
+            printf("COLD read U8    grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, bytes / t / 1e3);
+            t = time_it([&] { k_copy<4, false><<<gr, 256>>>(gs[k % NS], os[k % NS], n4); ++k; }, 40);
+            printf("COLD copy       grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 2 * bytes / t / 1e3);
+            t = time_it([&] { k_copy<4, true><<<gr, 256>>>(gs[k % NS], os[k % NS], n4); ++k; }, 40);
+            printf("COLD copy nt    grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 2 * bytes / t / 1e3);
+            t = time_it([&] { k_r1w2<4, false><<<gr, 256>>>(gs[k % NS], os[k % NS], n4); ++k; }, 40);
+            printf("COLD r1w2       grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 3 * bytes / t / 1e3);
+            t = time_it([&] { k_r1w2<4, true><<<gr, 256>>>(gs[k % NS], os[k % NS], n4); ++k; }, 40);
+            printf("COLD r1w2 nt    grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 3 * bytes / t / 1e3);
+        }
+        for (int gr : {4096, 8192}) {
+            float t = time_it([&] {
+                k_read<4><<<gr, 256>>>(gs[k % NS], sink, n4);
+                k_r1w2<4, false><<<gr, 256>>>(gs[k % NS], os[k % NS], n4);
+                ++k;
+            }, 40);
+            printf("COLD read+r1w2  grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 4 * bytes / t / 1e3);
+        }
+        for (int i = 0; i < NS; ++i) {
+            CK(hipFree(gs[i]));
+            CK(hipFree(os[i]));
+        }
+    }
     CK(hipDeviceSynchronize());
     return 0;
 }
