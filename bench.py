@@ -294,7 +294,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-        "data": f"synthetic N(0,1) gradients of the named parameter shapes (torch.randn on device), "
+        "data": "synthetic N(0,1) gradients of the named parameter shapes (torch.randn on device), " +
                 (f"{S} independent sets rotated per step (cold Infinity Cache)" if do_cold else "one set (warm)"),
         "config": {"workload": a.config, "rank": c["rank"], "num_iters_per_step": c["iters"],
                    "min_compression_rate": c["mcr"], "tensors": len(shapes),

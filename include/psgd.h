@@ -25,7 +25,10 @@
  *  - Ownership: the caller owns gradients, outputs, the P/Q state buffers and the workspace;
  *    the plan owns host-side layout only.
  *  - Gradients are mutated in place into the error-feedback residual (reference :230).
- *  - P/Q factors are always fp32 (reference :241-251 allocates them in the default dtype).
+ *  - P/Q factors are fp32 for fp32/bf16 gradients and fp64 for fp64 gradients (reference
+ *    :241-251 allocates them in the default dtype, which must match the gradients' for its bmm).
+ *  - The building blocks (psgd_product / psgd_orthogonalize / psgd_reconstruct) and the fused
+ *    fp32 kernels take fp32/bf16 plans only (PSGD_ERR_DTYPE for an F64 plan).
  *  - Errors: every call returns a psgd_status; psgd_last_error() returns a thread-local message.
  *    PSGD_ERR_INDEX mirrors the reference's IndexError (no tensors, :118), PSGD_ERR_DTYPE its
  *    RuntimeError on unsupported dtypes (:189), PSGD_ERR_LAYOUT its RuntimeError on
@@ -54,7 +57,10 @@ enum psgd_status {
     PSGD_ERR_STATE = 6    /* call order error (e.g. compute before psgd_plan_bind)  */
 };
 
-enum psgd_dtype { PSGD_F32 = 0, PSGD_BF16 = 1 };
+/* Gradient dtypes. F32 / BF16: factors (P/Q state) and arithmetic fp32. F64: the reference's
+ * own test dtype (tests/powersgd_test.py:38): factors and arithmetic fp64, as the reference's
+ * default-dtype P/Q (powersgd.py:241-251) are then. */
+enum psgd_dtype { PSGD_F32 = 0, PSGD_BF16 = 1, PSGD_F64 = 2 };
 
 /* Largest num_iters_per_step a plan accepts. */
 #define PSGD_MAX_ITERS 16
@@ -92,10 +98,10 @@ int psgd_plan_workspace_bytes(const psgd_plan* plan, int64_t* bytes);
 int psgd_plan_compression_rate(const psgd_plan* plan, double* rate, double* uncompressed,
                                double* compressed);
 
-/* Bind caller-owned device memory: P state [p_numel] fp32, Q state [q_numel] fp32 and a
- * workspace of psgd_plan_workspace_bytes() bytes (16-byte aligned). Uploads the static
- * layout tables (synchronous; call once). */
-int psgd_plan_bind(psgd_plan* plan, int32_t device, float* p_state, float* q_state,
+/* Bind caller-owned device memory: P state [p_numel] and Q state [q_numel] (fp32, or fp64
+ * for a PSGD_F64 plan) and a workspace of psgd_plan_workspace_bytes() bytes (16-byte
+ * aligned). Uploads the static layout tables (synchronous; call once). */
+int psgd_plan_bind(psgd_plan* plan, int32_t device, void* p_state, void* q_state,
                    void* workspace);
 
 /* Which state buffer iteration `it` of step `step` produces (and the caller must SUM-

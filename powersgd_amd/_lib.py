@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # PSGD_LIB_PATH: an alternative in-tree build (tuning variants); default the standard one
 LIB_PATH = os.environ.get("PSGD_LIB_PATH") or os.path.join(_HERE, "_lib", "libpsgd.so")
 
-PSGD_F32, PSGD_BF16 = 0, 1
+PSGD_F32, PSGD_BF16, PSGD_F64 = 0, 1, 2
 _STATUS_NAMES = {1: "INDEX", 2: "VALUE", 3: "DTYPE", 4: "LAYOUT", 5: "DEVICE", 6: "STATE"}
 
 _i32, _i64, _dbl, _vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p

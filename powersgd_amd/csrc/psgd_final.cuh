@@ -45,6 +45,15 @@ struct FinNT {
 // slot past the row end or past the matrix gets offset kOob, which loads 0 and drops the
 // store in hardware (no clamping, no branches). The plan keeps a fused matrix below 2^31
 // bytes.
+// Store cache policy of the streaming outputs (residual, output): 2 = nt (gfx950 CPol:
+// sc0 = 1, nt = 2, sc1 = 16), 0 = default. nt keeps the 204 MB a ResNet-50 final pass writes
+// from sitting dirty in the Infinity Cache, where their write-back competed with the NEXT
+// step's cold gradient reads: the even product took 33 us after default-policy stores, 28 us
+// after nt ones (profiles/r02/ab_nt). Build-time knob for A/B runs.
+#ifndef PSGD_ST_AUX
+#define PSGD_ST_AUX 2
+#endif
+
 template <typename T>
 struct FinIo;
 
@@ -53,10 +62,10 @@ struct FinIo<float> {
     static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const v4u x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, PSGD_ST_AUX);
     }
     static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, PSGD_ST_AUX);
     }
 };
 
@@ -66,10 +75,10 @@ struct FinIo<bf16_t> {
         typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
         const v2u_ x = {uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
                         uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, PSGD_ST_AUX);
     }
     static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, PSGD_ST_AUX);
     }
 };
 

@@ -176,6 +176,48 @@ struct OrthArgs {
     int32_t flags;       // diagnostics (PSGD_ORTH_DIAG): 1 = skip the Householder fallback
 };
 
+// ------------------------------------------------------------------ fp64 gradients
+// The reference's own error-feedback test runs in float64 (tests/powersgd_test.py:38); its P/Q
+// then follow the default dtype (powersgd.py:241-251), so gradients, factors and arithmetic are
+// all fp64 (psgd_f64.hip). Same plan layout (MatDesc, OrthUnit, P/Q offsets) as fp32.
+constexpr int kF64Cols = 64;    // even product: columns per tile (one per lane)
+constexpr int kF64Rows = 256;   // even product: rows per chunk (partials per chunk)
+constexpr int kF64OddRows = 16; // odd product: rows per workgroup (4 per wave)
+
+struct TermsF64 {
+    const double* p[kMaxTerms];
+    const double* q[kMaxTerms];
+};
+
+struct F64Args {
+    const MatDesc* mats;
+    const Tile* tiles;
+    void* const* grads;       // G_0 (in), residual (out, apply)
+    const double* x;          // orthonormal in-factor (products)
+    double* part;             // even partials [nchunk][m][r] per matrix at part_off[mat]
+    const int64_t* part_off;
+    double* y;                // out-factor state (reduce / odd product)
+    double* yh;               // its history copy
+    TermsF64 res;             // local terms (products: earlier iterations; apply: all)
+    int32_t nres;
+    TermsF64 apx;             // all-reduced terms (apply), scaled by alpha
+    double alpha;
+    void* out;                // flat output (apply)
+    const RedItem* items;     // even reduction items
+};
+
+struct F64OrthArgs {
+    const OrthUnit* units;
+    double* state;            // in-factor, orthonormalised in place
+    double* hx;               // history copy of the result
+    double* save;             // if non-null: copy of the values before orthonormalisation
+};
+
+hipError_t launch_f64_product(bool even, int R, const F64Args& a, int ntiles, hipStream_t s);
+hipError_t launch_f64_reduce(int R, const F64Args& a, int nitems, hipStream_t s);
+hipError_t launch_f64_apply(int R, const F64Args& a, int ntiles, hipStream_t s);
+hipError_t launch_f64_orth(int R, const F64OrthArgs& a, int nunits, hipStream_t s);
+
 // Host-side launchers (psgd_kernels*.hip). Return hipError_t.
 hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a,
                           int ntiles, hipStream_t s);
@@ -192,5 +234,6 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, h
 // paper-code Gram-Schmidt (gradient_reducers.py:945-956) on one panel per unit, per matrix
 hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
+hipError_t launch_flat_pack_f64(const FlatArgs& a, hipStream_t s);
 
 }  // namespace psgd

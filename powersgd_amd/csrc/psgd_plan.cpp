@@ -351,6 +351,12 @@ struct psgd_plan {
     // even product, and per group the [begin, end) slot range
     std::vector<int32_t> ss0_base, grng_ss0;
     int64_t ss0_slots = 0;
+    // fp64 plans (psgd_f64.hip): even tiles (64-column strip, 256-row chunk), odd tiles
+    // (16-row blocks), apply tiles (row chunks of ~16k elements), even partial offsets
+    std::vector<Tile> f64_even, f64_odd, f64_apply;
+    std::vector<int64_t> f64_part_off;
+    int64_t f64_part = 0;
+    size_t o_f64_even = 0, o_f64_odd = 0, o_f64_apply = 0, o_f64_partoff = 0, o_f64_part = 0;
     bool bound = false;
     int device = -1;
     float* P = nullptr;
@@ -371,6 +377,31 @@ struct psgd_plan {
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
         return reinterpret_cast<float*>(ws + o_hist) + (int64_t(which) * iters + k) * fmax;
+    }
+    double* hist64(int which, int k) const {  // the same history, fp64 plans
+        return reinterpret_cast<double*>(ws + o_hist) + (int64_t(which) * iters + k) * fmax;
+    }
+    bool f64() const { return dtype == PSGD_F64; }
+    void set_f64_tiles() {
+        f64_even.clear();
+        f64_odd.clear();
+        f64_apply.clear();
+        f64_part_off.clear();
+        f64_part = 0;
+        vec_now = base_vec;
+        for (size_t i = 0; i < mats.size(); ++i) {
+            MatDesc& d = mats[i];
+            d.vec = 0;
+            d.nstrip = int32_t((d.m + kF64Cols - 1) / kF64Cols);
+            d.nchunk = int32_t((d.n + kF64Rows - 1) / kF64Rows);
+            d.chunk_rows = int32_t(std::max<int64_t>(1, 16384 / d.m));  // apply: ~16k elements per tile
+            for (int c = 0; c < d.nchunk; ++c)
+                for (int st = 0; st < d.nstrip; ++st) f64_even.push_back(Tile{int32_t(i), st, c, 0});
+            for (int64_t b = 0; b * kF64OddRows < d.n; ++b) f64_odd.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
+            for (int64_t b = 0; b * d.chunk_rows < d.n; ++b) f64_apply.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
+            f64_part_off.push_back(f64_part);
+            f64_part += int64_t(d.nchunk) * kWaves * d.m * d.r;
+        }
     }
     template <typename T>
     T* dev(size_t off) const { return reinterpret_cast<T*>(ws + off); }
@@ -604,7 +635,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     if (num_tensors < 1 || !dims || !ndims) return fail(PSGD_ERR_INDEX, "list index out of range (no tensors)");
     if (rank < 1) return fail(PSGD_ERR_VALUE, "rank must be >= 1");
     if (iters < 1 || iters > PSGD_MAX_ITERS) return fail(PSGD_ERR_VALUE, "num_iters_per_step must be in [1, 16]");
-    if (dtype != PSGD_F32 && dtype != PSGD_BF16) return fail(PSGD_ERR_DTYPE, "dtype must be fp32 or bf16");
+    if (dtype != PSGD_F32 && dtype != PSGD_BF16 && dtype != PSGD_F64)
+        return fail(PSGD_ERR_DTYPE, "dtype must be fp32, bf16 or fp64");
 
     auto* p = new psgd_plan();
     p->rank = rank;
@@ -702,7 +734,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
             md.tensor = g.tensors[b];
             md.group = int(gi);
             p->mats.push_back(md);
-            p->base_vec.push_back((g.m % 4 == 0 && g.r <= 8 && md.out_off % 4 == 0) ? 1 : 0);
+            p->base_vec.push_back((dtype != PSGD_F64 && g.m % 4 == 0 && g.r <= 8 && md.out_off % 4 == 0) ? 1 : 0);
         }
         poff += int64_t(g.tensors.size()) * g.n * g.r;
         qoff += int64_t(g.tensors.size()) * g.m * g.r;
@@ -762,7 +794,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->ss0_slots += std::max(a.nchunk, b.nchunk);  // unused slots stay zero (bind)
         p->grng_ss0.back() = int32_t(p->ss0_slots);
     }
-    p->set_vec(p->base_vec);
+    if (p->f64())
+        p->set_f64_tiles();  // fp64: its own kernels and tiles (psgd_f64.hip), no fused forms
+    else
+        p->set_vec(p->base_vec);
 
     size_t off = 0;
     auto carve = [&](size_t bytes) {
@@ -795,7 +830,12 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float));
     p->o_ss0_base = carve(std::max<size_t>(p->ss0_base.size(), 1) * sizeof(int32_t));
     p->o_grng_ss0 = carve(std::max<size_t>(p->grng_ss0.size(), 1) * sizeof(int32_t));
-    p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * sizeof(float));
+    p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * (p->f64() ? sizeof(double) : sizeof(float)));
+    p->o_f64_even = carve(std::max<size_t>(p->f64_even.size(), 1) * sizeof(Tile));
+    p->o_f64_odd = carve(std::max<size_t>(p->f64_odd.size(), 1) * sizeof(Tile));
+    p->o_f64_apply = carve(std::max<size_t>(p->f64_apply.size(), 1) * sizeof(Tile));
+    p->o_f64_partoff = carve(std::max<size_t>(p->f64_part_off.size(), 1) * sizeof(int64_t));
+    p->o_f64_part = carve(size_t(std::max<int64_t>(p->f64_part, 1)) * sizeof(double));
     p->o_part = carve(size_t(p->part_floats) * sizeof(float));
     p->ws_bytes = off;
     *out_plan = p;
@@ -856,13 +896,13 @@ int psgd_plan_compression_rate(const psgd_plan* p, double* rate, double* unc, do
     return PSGD_OK;
 }
 
-int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* workspace) {
+int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspace) {
     if (!p || !P || !Q || !workspace) return fail(PSGD_ERR_VALUE, "null argument");
     if (reinterpret_cast<uintptr_t>(workspace) % 16) return fail(PSGD_ERR_LAYOUT, "workspace must be 16-byte aligned");
     DevScope scope(device);
     p->device = device;
-    p->P = P;
-    p->Q = Q;
+    p->P = static_cast<float*>(P);  // fp64 plans: double buffers (see P64/Q64)
+    p->Q = static_cast<float*>(Q);
     p->ws = static_cast<char*>(workspace);
     const size_t nt = p->shapes.size();
     p->grad_tab.bind(p->dev<char>(p->o_ptrs), nt);
@@ -880,6 +920,13 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, float* P, float* Q, void* works
     if (int st = upload(p->dev<void>(p->o_ss0_base), p->ss0_base.data(), p->ss0_base.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_ss0), p->grng_ss0.data(), p->grng_ss0.size() * sizeof(int32_t))) return st;
     PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float)));
+    if (p->f64()) {
+        if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
+        if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
+        if (int st = upload(p->dev<void>(p->o_f64_apply), p->f64_apply.data(), p->f64_apply.size() * sizeof(Tile))) return st;
+        if (int st = upload(p->dev<void>(p->o_f64_partoff), p->f64_part_off.data(), p->f64_part_off.size() * sizeof(int64_t)))
+            return st;
+    }
     p->bound = true;
     return PSGD_OK;
 }
@@ -921,8 +968,82 @@ static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEv
     return PSGD_OK;
 }
 
+// ---------------------------------------------------------------- fp64 plans ------
+// The same iteration structure as the fp32 path below, on psgd_f64.hip's kernels: orthonormalise
+// the in-factor (saving the all-reduced values of the previous iteration), product with
+// G_k formed on the fly, and for even iterations the fixed-order partial reduction.
+static void fill_terms64(const psgd_plan* p, int64_t step, int count, TermsF64& res) {
+    for (int j = 0; j < count; ++j) {
+        const bool e = p->even(step, j);
+        res.p[j] = e ? p->hist64(0, j) : p->hist64(1, j);
+        res.q[j] = e ? p->hist64(1, j) : p->hist64(0, j);
+    }
+    for (int j = count; j < kMaxTerms; ++j) res.p[j] = res.q[j] = nullptr;
+}
+
+static int compress_f64(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s) {
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    const bool even = p->even(step, it);
+    double* P = reinterpret_cast<double*>(p->P);
+    double* Q = reinterpret_cast<double*>(p->Q);
+    double* in = even ? P : Q;
+    double* out = even ? Q : P;
+    F64OrthArgs oa{};
+    oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
+    oa.state = in;
+    oa.hx = p->hist64(0, it);
+    oa.save = it > 0 ? p->hist64(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
+    PSGD_HIP(launch_f64_orth(p->rbucket, oa, int(even ? p->units_p.size() : p->units_q.size()), s));
+    F64Args a{};
+    a.mats = p->dev<MatDesc>(p->o_mats);
+    a.grads = p->grad_tab.table();
+    a.x = p->hist64(0, it);
+    a.part = p->dev<double>(p->o_f64_part);
+    a.part_off = p->dev<int64_t>(p->o_f64_partoff);
+    a.y = out;
+    a.yh = p->hist64(1, it);
+    fill_terms64(p, step, it, a.res);
+    a.nres = it;
+    if (even) {
+        a.tiles = p->dev<Tile>(p->o_f64_even);
+        PSGD_HIP(launch_f64_product(true, p->rbucket, a, int(p->f64_even.size()), s));
+        a.items = p->dev<RedItem>(p->o_red_even);
+        PSGD_HIP(launch_f64_reduce(p->rbucket, a, int(p->red_even.size()), s));
+    } else {
+        a.tiles = p->dev<Tile>(p->o_f64_odd);
+        PSGD_HIP(launch_f64_product(false, p->rbucket, a, int(p->f64_odd.size()), s));
+    }
+    return PSGD_OK;
+}
+
+static int decompress_f64(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world, hipStream_t s) {
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    const int I = p->iters;
+    F64Args a{};
+    a.mats = p->dev<MatDesc>(p->o_mats);
+    a.tiles = p->dev<Tile>(p->o_f64_apply);
+    a.grads = p->grad_tab.table();
+    a.out = out;
+    fill_terms64(p, step, I, a.res);
+    double* last = reinterpret_cast<double*>(p->even(step, I - 1) ? p->Q : p->P);
+    for (int k = 0; k < I; ++k) {
+        const bool e = p->even(step, k);
+        double* ybar = k + 1 < I ? p->hist64(2, k) : last;  // all-reduced factor of iteration k
+        a.apx.p[k] = e ? p->hist64(0, k) : ybar;
+        a.apx.q[k] = e ? ybar : p->hist64(0, k);
+    }
+    a.nres = I;
+    a.alpha = 1.0 / double(world);  // reference alpha = 1 / num_workers (:218)
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (int st = timing_begin(p, s, &ev)) return st;
+    PSGD_HIP(launch_f64_apply(p->rbucket, a, int(p->f64_apply.size()), s));
+    if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
+    return PSGD_OK;
+}
+
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
                          bool fuse, bool write_out, const FlatArgs* fl = nullptr) {
+    if (p->f64()) return compress_f64(p, grads, step, it, s);
     if (int st = refresh_pointers(p, grads, s)) return st;
     const bool even = p->even(step, it);
     float* in = even ? p->P : p->Q;
@@ -1042,6 +1163,7 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
 
 static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
                            hipStream_t s, bool fuse, const FlatArgs* fl = nullptr) {
+    if (p->f64()) return decompress_f64(p, grads, out, step, world, s);
     if (int st = refresh_pointers(p, grads, s)) return st;
     const int I = p->iters;
     ApplyArgs aa{};
@@ -1097,6 +1219,7 @@ static int check_terms(int32_t nterms, const float* const* a, const float* const
 int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, float* y, int32_t nterms,
                  const float* const* term_p, const float* const* term_q, void* stream) {
     if (!p || !grads || !x || !y) return fail(PSGD_ERR_VALUE, "null argument");
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "the building blocks take fp32/bf16 plans");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (int st = check_terms(nterms, term_p, term_q)) return st;
     DevScope scope(p->device);
@@ -1141,6 +1264,7 @@ int psgd_orthogonalize(psgd_plan* p, int32_t which, float* buf, int32_t mode, vo
     if (!p || !buf) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (mode != 0 && mode != 1) return fail(PSGD_ERR_VALUE, "mode must be 0 (reference) or 1 (paper-code)");
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "the building blocks take fp32/bf16 plans");
     DevScope scope(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     OrthArgs oa{};
@@ -1176,6 +1300,7 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
     if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (nterms < 1) return fail(PSGD_ERR_VALUE, "at least one term");
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "the building blocks take fp32/bf16 plans");
     if (int st = check_terms(nterms, term_p, term_q)) return st;
     if (int st = check_terms(nterms, avg_p, avg_q)) return st;
     DevScope scope(p->device);
@@ -1259,7 +1384,8 @@ int psgd_flat_create(const int64_t* numels, int32_t count, int32_t dtype, psgd_f
     if (!out) return fail(PSGD_ERR_VALUE, "null argument");
     *out = nullptr;
     if (count < 0 || (count > 0 && !numels)) return fail(PSGD_ERR_VALUE, "bad tensor list");
-    if (dtype != PSGD_F32 && dtype != PSGD_BF16) return fail(PSGD_ERR_DTYPE, "dtype must be fp32 or bf16");
+    if (dtype != PSGD_F32 && dtype != PSGD_BF16 && dtype != PSGD_F64)
+        return fail(PSGD_ERR_DTYPE, "dtype must be fp32, bf16 or fp64");
     auto* f = new psgd_flat();
     f->dtype = dtype;
     f->count = count;
@@ -1340,7 +1466,7 @@ int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t ste
     if (!p->bound || !f->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
-    if (f->dtype != p->dtype || f->device != p->device) {  // separate launches
+    if (f->dtype != p->dtype || f->device != p->device || p->f64()) {  // separate launches
         if (int st = psgd_aggregate(p, grads, out, step, stream)) return st;
         return psgd_flat_pack(f, unc, flat_out, 1, stream);
     }

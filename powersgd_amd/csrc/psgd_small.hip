@@ -1608,6 +1608,7 @@ __global__ __launch_bounds__(kBlock) void k_flat_pack(FlatArgs a) {
 
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s) {
     if (a.nitems == 0) return hipSuccess;
+    if (dtype == 2) return launch_flat_pack_f64(a, s);
     if (dtype == 0)
         k_flat_pack<float><<<a.nitems, kBlock, 0, s>>>(a);
     else

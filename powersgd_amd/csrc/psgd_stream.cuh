@@ -61,6 +61,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 // exec-mask branch and a vmcnt(0) wait per load).
 __device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
 
+// streaming stores (residual, output, flat pack) with the nt cache policy; see PSGD_ST_AUX in
+// psgd_final.cuh for the measurement (build-time knob for A/B runs)
+#ifndef PSGD_NT_STORES
+#define PSGD_NT_STORES 1
+#endif
+
 template <typename T>
 struct Io;
 
@@ -73,7 +79,11 @@ struct Io<float> {
     static __device__ __forceinline__ void ld(gptr<const float> p, float (&v)[1]) { v[0] = *p; }
     static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[4]) {
         const v4f x = {v[0], v[1], v[2], v[3]};
+#if PSGD_NT_STORES
+        __builtin_nontemporal_store(x, (gptr<v4f>)p);
+#else
         *(gptr<v4f>)p = x;
+#endif
     }
     static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[1]) { *p = v[0]; }
 };
@@ -92,7 +102,11 @@ struct Io<bf16_t> {
         v2u x;
         x.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
         x.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+#if PSGD_NT_STORES
+        __builtin_nontemporal_store(x, (gptr<v2u>)p);
+#else
         *(gptr<v2u>)p = x;
+#endif
     }
     static __device__ __forceinline__ void st(gptr<bf16_t> p, const float (&v)[1]) { *p = f2bf(v[0]); }
 };
@@ -272,6 +286,16 @@ __device__ __forceinline__ TileGeom tile_geom(const MatDesc& d, const Tile& t) {
 }
 
 constexpr int kUnroll = 4;  // rows in flight per lane
+// products: rows per batch and whether the next batch is issued before the current one is
+// consumed (software pipeline); build-time knobs for A/B runs (Makefile EXTRA=-D...)
+#ifndef PSGD_PROD_UNROLL
+#define PSGD_PROD_UNROLL 4
+#endif
+#ifndef PSGD_PROD_PIPE
+#define PSGD_PROD_PIPE 0
+#endif
+constexpr int kProdUnroll = PSGD_PROD_UNROLL;
+constexpr bool kProdPipe = PSGD_PROD_PIPE != 0;
 
 // ------------------------------------------------- odd product, row layout (VALU) --
 // For full-width strips (256 columns = 64 lanes x 4) and r <= 4: a wave takes 16 rows; each
@@ -478,69 +502,78 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 #pragma unroll
         for (int c = 0; c < R; ++c) acc[v][c] = 0.f;
 
-    for (int64_t row = g.first_row; row < g.row_end; row += kUnroll * g.stride) {
-        float x[kUnroll][V];
-        int64_t rc[kUnroll];
-        // the rows' factor values (in-factor rows for the even product, error-feedback rows)
-        // are loaded together with the gradient rows: loaded inside the row loop they were a
-        // chain of kUnroll dependent round trips per batch
-        float xpu[EVEN ? kUnroll : 1][R];
-        float apu[KC][kUnroll][R];
+    // Software pipeline: batch b+1's gradient rows and factor rows are issued before batch b
+    // is consumed, so a lane keeps 2 x kProdUnroll 16-byte loads in flight. Loads are
+    // unconditional from clamped rows (a batch past the chunk re-reads its first rows, which
+    // hit L2). Cold gradients (HBM latency rather than Infinity-Cache latency) need the depth.
+    struct Batch {
+        float x[kProdUnroll][V];
+        int64_t rc[kProdUnroll];
+        float xpu[EVEN ? kProdUnroll : 1][R];
+        float apu[KC][kProdUnroll][R];
+    };
+    const int64_t step = int64_t(kProdUnroll) * g.stride;
+    auto load = [&](Batch& b, int64_t row) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kProdUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
-            rc[u] = rr < g.row_end ? rr : g.row_begin;  // clamped: every load is in range
-            Io<T>::ld(G + rc[u] * g.m + g.ccol, x[u]);
+            b.rc[u] = rr < g.row_end ? rr : g.row_begin;  // clamped: every load is in range
+            Io<T>::ld(G + b.rc[u] * g.m + g.ccol, b.x[u]);
         }
+        // the rows' factor values (in-factor rows for the even product, error-feedback rows)
+        // travel with the gradient rows (loaded inside the row loop they were a chain of
+        // dependent round trips per batch)
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const int32_t prow = int32_t(rc[u]) * r;
-            if constexpr (EVEN) ld_factor<R>(xp_base + prow, r, xpu[u]);
+        for (int u = 0; u < kProdUnroll; ++u) {
+            const int32_t prow = int32_t(b.rc[u]) * r;
+            if constexpr (EVEN) ld_factor<R>(xp_base + prow, r, b.xpu[u]);
             if constexpr (K > 0) {
 #pragma unroll
-                for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, apu[k][u]);
+                for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, b.apu[k][u]);
             }
         }
+    };
+    auto process = [&](Batch& b, int64_t row) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kProdUnroll; ++u) {
             const bool valid = g.active && (row + u * g.stride) < g.row_end;
-            const int32_t prow = int32_t(rc[u]) * r;
+            const int32_t prow = int32_t(b.rc[u]) * r;
             // error feedback of the previous iterations, formed on the fly
             for (int k = 0; k < nres; ++k) {
                 float ap[R];
                 if constexpr (K > 0) {
 #pragma unroll
-                    for (int c = 0; c < R; ++c) ap[c] = apu[k < KC ? k : 0][u][c];
+                    for (int c = 0; c < R; ++c) ap[c] = b.apu[k < KC ? k : 0][u][c];
                 } else {
                     ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
                 }
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
-                    float b[R];
+                    float bb[R];
                     if constexpr (K > 0) {
 #pragma unroll
-                        for (int c = 0; c < R; ++c) b[c] = bq[k < KC ? k : 0][v][c];
+                        for (int c = 0; c < R; ++c) bb[c] = bq[k < KC ? k : 0][v][c];
                     } else {
-                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, b);
+                        ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bb);
                     }
-                    x[u][v] = x[u][v] - dotr<R>(ap, b);
+                    b.x[u][v] = b.x[u][v] - dotr<R>(ap, bb);
                 }
             }
 #pragma unroll
-            for (int v = 0; v < V; ++v) x[u][v] = valid ? x[u][v] : 0.f;
+            for (int v = 0; v < V; ++v) b.x[u][v] = valid ? b.x[u][v] : 0.f;
             if constexpr (EVEN) {
 #pragma unroll
                 for (int v = 0; v < V; ++v)
 #pragma unroll
-                    for (int c = 0; c < R; ++c) acc[v][c] = fmaf(x[u][v], xpu[u][c], acc[v][c]);
+                    for (int c = 0; c < R; ++c) acc[v][c] = fmaf(b.x[u][v], b.xpu[u][c], acc[v][c]);
             } else {
                 float dot[R];
 #pragma unroll
                 for (int c = 0; c < R; ++c) {
-                    float s = x[u][0] * xq[0][c];
+                    float sacc = b.x[u][0] * xq[0][c];
 #pragma unroll
-                    for (int v = 1; v < V; ++v) s = fmaf(x[u][v], xq[v][c], s);
-                    dot[c] = sum_within(s, g.L);
+                    for (int v = 1; v < V; ++v) sacc = fmaf(b.x[u][v], xq[v][c], sacc);
+                    dot[c] = sum_within(sacc, g.L);
                 }
                 const int64_t rr = row + u * g.stride;
                 if (g.ql == 0 && rr < g.row_end) {
@@ -550,6 +583,22 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                         if (c < r) dst[c] = dot[c];
                 }
             }
+        }
+    };
+    if constexpr (kProdPipe) {
+        Batch cur;
+        load(cur, g.first_row);
+        for (int64_t row = g.first_row; row < g.row_end; row += step) {
+            Batch nxt;
+            load(nxt, row + step);  // issued before cur is consumed (no keep(): that would wait)
+            process(cur, row);
+            cur = nxt;
+        }
+    } else {
+        for (int64_t row = g.first_row; row < g.row_end; row += step) {
+            Batch cur;
+            load(cur, row);
+            process(cur, row);
         }
     }
 

@@ -92,6 +92,6 @@ class PowerSGDState:
             fut.set_result(out)
 
 
-def powersgd_hook(state: PowerSGDState, bucket: "dist.GradBucket") -> "torch.futures.Future[torch.Tensor]":
+def powersgd_hook(state: PowerSGDState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
     """``DistributedDataParallel.register_comm_hook`` hook: the reference's PowerSGD flow."""
     return state._arrive(bucket)

@@ -14,6 +14,8 @@ Differences, all deliberate:
 * Device tensors on a ROCm GPU only; the HIP library is mandatory (no CPU fallback).
 * bfloat16 gradients are supported (the reference raises at its ``bmm``, :189): the
   gradient matrix is read/written in bf16, factors and arithmetic stay fp32.
+* float64 gradients (the reference's own test dtype) run fp64 kernels with fp64 factors; as in
+  the reference, torch's default dtype must then be float64 (P/Q follow it, :241-251).
 * Returned compressed outputs are views of one flat buffer (allocated fresh per call)
   instead of separate ``empty_like`` tensors; uncompressed outputs are views in the
   reference too.
@@ -39,7 +41,7 @@ except ImportError as e:  # built together with libpsgd.so; no Python fallback
         "`python -c 'import __graft_entry__ as g; g.build()'`"
     ) from e
 
-_DTYPES = {torch.float32: _lib.PSGD_F32, torch.bfloat16: _lib.PSGD_BF16}
+_DTYPES = {torch.float32: _lib.PSGD_F32, torch.bfloat16: _lib.PSGD_BF16, torch.float64: _lib.PSGD_F64}
 
 
 def _require_device(device: torch.device) -> int:
@@ -54,26 +56,20 @@ def _dtype_code(dtype: torch.dtype) -> int:
     try:
         return _DTYPES[dtype]
     except KeyError:
-        raise RuntimeError(f"powersgd_amd supports float32 and bfloat16 gradients, got {dtype}")
+        raise RuntimeError(f"powersgd_amd supports float32, bfloat16 and float64 gradients, got {dtype}")
 
 
 def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-class _OutputSlab:
-    """A FRESH flat output buffer + views per call, like the reference's per-call
-    ``empty_like`` (:153): a caller may keep last step's outputs (``p.grad = out``, tensors
-    saved by autograd) and they are never overwritten. The caching allocator hands back the
-    block of an output nobody holds any more, so this costs no device allocation in steady
-    state. ``flat`` is the buffer of the latest call."""
-
-    def __init__(self):
-        self.flat: Optional[torch.Tensor] = None
-
-    def get(self, numel: int, shapes: Sequence[torch.Size], dtype, device) -> List[torch.Tensor]:
-        self.flat = torch.empty(max(numel, 1), dtype=dtype, device=device)
-        return _views(self.flat, shapes)
+def _output_slab(shapes, code: int, dev_index: int):
+    """Flat output buffer + per-tensor views (csrc/psgd_host.cpp OutputSlab): ``get()`` returns
+    the views, handing the previous call's buffer out again only when no reference to any of
+    its views survives anywhere (TensorImpl, PyObject and storage reference counts back at
+    their creation values), else a fresh buffer, like the reference's per-call ``empty_like``
+    (:153). ``flat`` is the buffer of the latest call."""
+    return _psgd_host.OutputSlab([list(s) for s in shapes], code, dev_index)
 
 
 class Aggregator(ABC):
@@ -122,12 +118,12 @@ class _FlatEntry:
                        self.ws.data_ptr())
         self.ptrs = _lib.ptr_array([0] * len(self.shapes))
         self.ptr_addr = ctypes.addressof(self.ptrs)
-        self.slab = _OutputSlab()
+        self.slab = _output_slab(self.shapes, code, _require_device(device))
 
     def run(self, ptr_addr: int) -> List[torch.Tensor]:
-        outs = self.slab.get(self.numel, self.shapes, self.dtype, self.device)
+        outs = self.slab.get()
         world = torch.distributed.get_world_size() if is_distributed() else 1
-        self.plan.pack(ptr_addr, self.slab.flat.data_ptr(), world, _stream(self.device))
+        self.plan.pack(ptr_addr, self.slab.data_ptr(), world, _stream(self.device))
         if is_distributed():
             torch.distributed.all_reduce(self.slab.flat[:self.numel])
         return outs
@@ -185,9 +181,9 @@ class PowerSGD(Aggregator):
         elif self._unc is not None and not is_distributed():
             # world size 1: the uncompressed copy/zero rides in the codec's final launch
             u = self._unc
-            unc = u.slab.get(u.numel, u.shapes, u.dtype, self.device)
+            unc = u.slab.get()
             outs = self._powersgd._aggregate_table(self._table.comp_addr(),
-                                                   flat=(u.plan, self._table.unc_addr(), u.slab.flat.data_ptr()))
+                                                   flat=(u.plan, self._table.unc_addr(), u.slab.data_ptr()))
             outs = outs + unc
         else:
             outs = self._powersgd._aggregate_table(self._table.comp_addr())
@@ -208,7 +204,7 @@ class PowerSGD(Aggregator):
         world = torch.distributed.get_world_size()
         self._unc.plan.pack(self._table.unc_addr(), tail.data_ptr(), world, _stream(self.device))
         outs = codec._aggregate_table(self._table.comp_addr(), last_comm=comm)
-        unc = self._unc.slab.get(self._unc.numel, self._unc.shapes, self._unc.dtype, self.device)
+        unc = self._unc.slab.get()
         self._unc.slab.flat[:self._unc.numel].copy_(tail)
         return outs + unc
 
@@ -263,14 +259,21 @@ class BasicPowerSGD(Aggregator):
         self._qs = _views(self._qs_buffer, [b.shape for b in q_batches])
         pn, qn = self._plan.factor_numel()
         assert pn == self._ps_buffer.numel() and qn == self._qs_buffer.numel()
-        if self._ps_buffer.dtype != torch.float32:
-            raise RuntimeError("powersgd_amd keeps P/Q in float32 (torch default dtype must be float32)")
+        # P/Q follow torch's default dtype, as in the reference (:241-251), whose bmm then needs
+        # the gradients in that dtype (fp64 tests: torch.set_default_dtype(torch.float64),
+        # tests/powersgd_test.py:38). bf16 gradients keep fp32 factors (the reference raises).
+        want = torch.float64 if self.dtype == torch.float64 else torch.float32
+        if self._ps_buffer.dtype != want:
+            names = {torch.float64: "Double", torch.float32: "Float"}
+            raise RuntimeError(f"expected scalar type {names[want]} but found "
+                               f"{names.get(self._ps_buffer.dtype, self._ps_buffer.dtype)} (P/Q follow torch's "
+                               f"default dtype; gradients are {self.dtype})")
         self._workspace = torch.empty(self._plan.workspace_bytes(), dtype=torch.uint8, device=self.device)
         self._plan.bind(self._dev_index, self._ps_buffer.data_ptr(), self._qs_buffer.data_ptr(),
                         self._workspace.data_ptr())
         self._out_numel = self._plan.output_numel()
         self._shapes = [p.shape for p in self.params]
-        self._slab = _OutputSlab()
+        self._slab = _output_slab(self._shapes, self._code, self._dev_index)
         self._table = _psgd_host.PtrTable([list(s) for s in self._shapes], [True] * len(self._shapes),
                                           self._code, self._dev_index)
         self._p_comm: Optional[torch.Tensor] = None
@@ -310,8 +313,8 @@ class BasicPowerSGD(Aggregator):
         ``last_comm``: all-reduce this [factor | tail] buffer in place of the last factor.
         ``flat``: (FlatPlan, uncompressed pointer table, flat output pointer) packed in the
         same final launch (world size 1, psgd_aggregate_flat)."""
-        outs = self._slab.get(self._out_numel, self._shapes, self.dtype, self.device)
-        out_ptr = self._slab.flat.data_ptr()
+        outs = self._slab.get()
+        out_ptr = self._slab.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
         if is_distributed():

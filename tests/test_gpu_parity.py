@@ -9,9 +9,10 @@
 
 Tolerances (fp32 floating point; north_star asks for a stated fp32 tolerance): per
 tensor ||ours - ref||_F <= TOL * ||input||_F with TOL_STEP = 1e-5 per step from an
-identical state and TOL_FREE = 1e-4 for up to 4 free-running steps; bf16 gradients
-(reference cannot run them) compare against the oracle on bf16-rounded inputs with
-TOL_BF16 = 1e-2.
+identical state (TOL_STEP_R1 = 1e-6 at rank 1) and TOL_FREE = 1e-4 for up to 4
+free-running steps; bf16 gradients (reference cannot run them) compare against the oracle
+on bf16-rounded inputs with TOL_BF16 = 1e-2. Every comparison's error is logged
+(tests/parity_log.py); DESIGN.md §5 quotes the worst observed values.
 """
 import os
 
@@ -28,6 +29,7 @@ from powersgd_amd.workloads import CONFIGS, hash_tensors, resnet50_shapes
 pytestmark = pytest.mark.gpu
 
 TOL_STEP = 1e-5
+TOL_STEP_R1 = 1e-6  # rank 1: same op order as the reference up to summation order
 TOL_FREE = 1e-4
 TOL_BF16 = 1e-2
 DEV = torch.device("cuda:0")
@@ -61,6 +63,7 @@ def test_golden_per_step(name):
     shapes = [tuple(s) for s in meta["shapes"]]
     psgd = _new_gpu(meta)
     assert psgd.is_compressed_mask == list(want["mask"])
+    tol = TOL_STEP_R1 if meta["rank"] == 1 else TOL_STEP
     res_ref = [torch.zeros(s) for s in shapes]
     for t in range(meta["steps"]):
         if t == 0:
@@ -74,8 +77,8 @@ def test_golden_per_step(name):
         for i, g in enumerate(inputs):
             wo = torch.from_numpy(want[f"s{t}_out_{i}"])
             wr = torch.from_numpy(want[f"s{t}_res_{i}"])
-            check(_rel(outs[i], wo, g), TOL_STEP, name, t, i, "out")
-            check(_rel(grads[i], wr, g), TOL_STEP, name, t, i, "res")
+            check(_rel(outs[i], wo, g), tol, name, t, i, "out")
+            check(_rel(grads[i], wr, g), tol, name, t, i, "res")
         assert [psgd.step_counter, psgd._powersgd.step_counter] == list(want[f"s{t}_step"])
         res_ref = [torch.from_numpy(want[f"s{t}_res_{i}"]) for i in range(len(shapes))]
 
@@ -165,7 +168,8 @@ def _oracle_and_gpu(cfg, steps, dtype=torch.float32):
 def test_baseline_configs_vs_oracle(cfg):
     steps = 3
     for t, inputs, og, oc, rg, rc in _oracle_and_gpu(cfg, steps):
-        tol = TOL_STEP * 4 if t == 0 else TOL_FREE
+        # step 0 starts from the oracle's own state: per-step bound; later steps free-running
+        tol = (TOL_STEP_R1 if CONFIGS[cfg]["rank"] == 1 else TOL_STEP) if t == 0 else TOL_FREE
         for i, g in enumerate(inputs):
             check(_rel(og[i], oc[i], g), tol, cfg, t, i, "out")
             check(_rel(rg[i], rc[i], g), tol, cfg, t, i, "res")

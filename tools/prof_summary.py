@@ -58,8 +58,10 @@ def main():
                     traffic[c + "_prio"] = prio
     if "--traffic" in sys.argv and "FETCH_SIZE" in traffic and "WRITE_SIZE" in traffic:
         cfg = sys.argv[sys.argv.index("--traffic") + 1]
-        out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                           "pmc_traffic.json")
+        # on the GPU box only gpurun_out/ travels back: write there (tools/merge_traffic.py
+        # folds it into the committed profiles/pmc_traffic.json)
+        out = os.environ.get("PSGD_TRAFFIC_OUT") or os.path.join(
+            os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "pmc_traffic.json")
         try:
             data = json.load(open(out))
         except (OSError, ValueError):
