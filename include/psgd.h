@@ -12,6 +12,8 @@
  *                           local error-feedback update :195-202)
  *   psgd_decompress        approximation + un-batching  powersgd/powersgd.py:211-230
  *   psgd_plan_fused_final  (which final-pass form a step takes; no reference counterpart)
+ *   psgd_*_bucket          the same per bucket of shape groups, for comm/compute overlap of the
+ *                          factor all-reduce (powersgd.py:204-209 split into slices)
  *   psgd_aggregate         BasicPowerSGD.aggregate      powersgd/powersgd.py:146-235 (world size 1)
  *   psgd_flat_*            AllReduce.aggregate          powersgd/powersgd.py:22-31,
  *                          pack / allreduce_average      powersgd/utils.py:6-10, :43-49
@@ -126,6 +128,24 @@ int psgd_compress(psgd_plan* plan, void* const* grads, int64_t step, int32_t it,
  * all-reduce). */
 int psgd_decompress(psgd_plan* plan, void* const* grads, void* out, int64_t step,
                     int32_t world_size, void* stream);
+
+/* ------------------------------------------- buckets: comm/compute overlap (W > 1) ------ */
+/* The reference all-reduces the whole out-factor buffer once per iteration (powersgd.py:
+ * 204-209). With buckets, the shape groups are cut into `nbuckets` consecutive ranges
+ * (group_end[b] = exclusive end group; the last must be psgd_plan_num_groups) and every launch of
+ * an iteration can be issued per bucket: the caller all-reduces bucket b's slice of the factor
+ * buffer (psgd_plan_bucket_range: element offset/length in the P and Q state buffers) as soon
+ * as bucket b's kernels are queued, so that collective overlaps the next buckets' kernels. The
+ * element-wise SUM over the slices equals the whole-buffer SUM. nbuckets = 0: one bucket (the
+ * whole plan). Synchronous (rewrites the tile tables): call between steps. fp32/bf16 plans. */
+int psgd_plan_set_buckets(psgd_plan* plan, int32_t nbuckets, const int32_t* group_end);
+int psgd_plan_bucket_range(const psgd_plan* plan, int32_t bucket, int64_t* p_off, int64_t* p_len,
+                           int64_t* q_off, int64_t* q_len);
+/* psgd_compress / psgd_decompress restricted to one bucket's matrices (same semantics). */
+int psgd_compress_bucket(psgd_plan* plan, void* const* grads, int64_t step, int32_t it, int32_t bucket,
+                         void* stream);
+int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64_t step,
+                           int32_t world_size, int32_t bucket, void* stream);
 
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);

@@ -49,6 +49,10 @@ _SIGNATURES = {
     "psgd_product": ([_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp], _i32),
     "psgd_orthogonalize": ([_vp, _i32, _vp, _i32, _vp], _i32),
     "psgd_reconstruct": ([_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, ctypes.c_float, _vp], _i32),
+    "psgd_plan_set_buckets": ([_vp, _i32, _P_i32], _i32),
+    "psgd_plan_bucket_range": ([_vp, _i32, _P_i64, _P_i64, _P_i64, _P_i64], _i32),
+    "psgd_compress_bucket": ([_vp, _vp, _i64, _i32, _i32, _vp], _i32),
+    "psgd_decompress_bucket": ([_vp, _vp, _vp, _i64, _i32, _i32, _vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -178,6 +182,23 @@ class Plan:
     def aggregate_flat(self, grads, out_ptr: int, step: int, flat: "FlatPlan", unc, flat_out: int,
                        stream: int) -> None:
         check(lib().psgd_aggregate_flat(self._h, grads, out_ptr, step, flat._h, unc, flat_out, stream))
+
+    # --- buckets of shape groups (W > 1 comm/compute overlap)
+    def set_buckets(self, group_end: Sequence[int]) -> None:
+        arr = (_i32 * max(1, len(group_end)))(*group_end)
+        check(lib().psgd_plan_set_buckets(self._h, len(group_end), arr))
+
+    def bucket_range(self, b: int):
+        po, pl, qo, ql = _i64(), _i64(), _i64(), _i64()
+        check(lib().psgd_plan_bucket_range(self._h, b, ctypes.byref(po), ctypes.byref(pl), ctypes.byref(qo),
+                                           ctypes.byref(ql)))
+        return po.value, pl.value, qo.value, ql.value
+
+    def compress_bucket(self, grads, step: int, it: int, bucket: int, stream: int) -> None:
+        check(lib().psgd_compress_bucket(self._h, grads, step, it, bucket, stream))
+
+    def decompress_bucket(self, grads, out_ptr: int, step: int, world: int, bucket: int, stream: int) -> None:
+        check(lib().psgd_decompress_bucket(self._h, grads, out_ptr, step, world, bucket, stream))
 
     def fused_final(self, step: int) -> bool:
         """True when the last iteration of ``step`` runs fused with the final pass."""

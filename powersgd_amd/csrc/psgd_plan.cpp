@@ -351,6 +351,65 @@ struct psgd_plan {
     // even product, and per group the [begin, end) slot range
     std::vector<int32_t> ss0_base, grng_ss0;
     int64_t ss0_slots = 0;
+    // Buckets of whole shape groups (W > 1 overlap, psgd_plan_set_buckets): per bucket the
+    // [begin, end) range of every launch list (all are in matrix order) and of the P/Q buffers.
+    struct Span {
+        int32_t tiles[2], ov[2], om[2], fin[2], re[2], ro[2], up[2], uq[2];
+        int64_t p[2], q[2];
+    };
+    std::vector<int32_t> bucket_gend;              // exclusive group end per bucket
+    std::vector<Span> spans;
+    std::vector<int32_t> unit_group_p, unit_group_q;
+    Span full_span() const {
+        Span sp{};
+        sp.tiles[1] = int32_t(tiles.size());
+        sp.ov[1] = int32_t(tiles_ov.size());
+        sp.om[1] = int32_t(tiles_om.size());
+        sp.fin[1] = int32_t(tiles_fin.size());
+        sp.re[1] = int32_t(red_even.size());
+        sp.ro[1] = int32_t(red_odd.size());
+        sp.up[1] = int32_t(units_p.size());
+        sp.uq[1] = int32_t(units_q.size());
+        sp.p[1] = ptot;
+        sp.q[1] = qtot;
+        return sp;
+    }
+    void build_spans() {
+        spans.clear();
+        int32_t g0 = 0;
+        for (size_t b = 0; b < bucket_gend.size(); ++b) {
+            const int32_t g1 = bucket_gend[b];
+            auto in = [&](int32_t mat) { const int32_t g = mats[mat].group; return g >= g0 && g < g1; };
+            auto range = [&](const auto& v, auto key, int32_t (&r)[2]) {
+                r[0] = int32_t(v.size());
+                r[1] = 0;
+                for (size_t i = 0; i < v.size(); ++i)
+                    if (key(v[i])) {
+                        r[0] = std::min(r[0], int32_t(i));
+                        r[1] = int32_t(i) + 1;
+                    }
+                if (r[1] == 0) r[0] = 0;
+            };
+            Span sp{};
+            auto tk = [&](const Tile& t) { return in(t.mat); };
+            auto rk = [&](const RedItem& it) { return in(it.mat); };
+            range(tiles, tk, sp.tiles);
+            range(tiles_ov, tk, sp.ov);
+            range(tiles_om, tk, sp.om);
+            range(tiles_fin, tk, sp.fin);
+            range(red_even, rk, sp.re);
+            range(red_odd, rk, sp.ro);
+            range(unit_group_p, [&](int32_t g) { return g >= g0 && g < g1; }, sp.up);
+            range(unit_group_q, [&](int32_t g) { return g >= g0 && g < g1; }, sp.uq);
+            sp.p[0] = groups[g0].poff;
+            sp.q[0] = groups[g0].qoff;
+            sp.p[1] = g1 < int32_t(groups.size()) ? groups[g1].poff : ptot;
+            sp.q[1] = g1 < int32_t(groups.size()) ? groups[g1].qoff : qtot;
+            spans.push_back(sp);
+            g0 = g1;
+        }
+    }
+
     // fp64 plans (psgd_f64.hip): even tiles (64-column strip, 256-row chunk), odd tiles
     // (16-row blocks), apply tiles (row chunks of ~16k elements), even partial offsets
     std::vector<Tile> f64_even, f64_odd, f64_apply;
@@ -512,7 +571,7 @@ struct psgd_plan {
         // Optional: largest tiles first (a greedy longest-processing-time order for the
         // dispatcher, which hands out workgroups in index order as slots free up).
         // Measured neutral-to-worse on ResNet-50 (profiles/r01), so off by default.
-        if (env_int("PSGD_SORT_TILES", 0)) {
+        if (env_int("PSGD_SORT_TILES", 0) && bucket_gend.empty()) {  // buckets need matrix order
             auto cost_fin = [&](const Tile& t) {
                 const MatDesc& d = mats[t.mat];
                 return std::min<int64_t>(d.fin_rows, d.n - int64_t(t.chunk) * d.fin_rows) * d.m;
@@ -530,6 +589,7 @@ struct psgd_plan {
             std::stable_sort(tiles.begin(), tiles.end(), by(cost_col));
             std::stable_sort(tiles_ov.begin(), tiles_ov.end(), by(cost_col));
         }
+        if (!bucket_gend.empty()) build_spans();
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits)
     bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
@@ -742,10 +802,14 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         if (g.r == 1) {
             p->units_p.push_back(OrthUnit{g.poff, g.n, 1, int32_t(g.tensors.size())});
             p->units_q.push_back(OrthUnit{g.qoff, g.m, 1, int32_t(g.tensors.size())});
+            p->unit_group_p.push_back(int32_t(gi));
+            p->unit_group_q.push_back(int32_t(gi));
         } else {
             for (size_t b = 0; b < g.tensors.size(); ++b) {
                 p->units_p.push_back(OrthUnit{g.poff + int64_t(b) * g.n * g.r, g.n, g.r, 1});
                 p->units_q.push_back(OrthUnit{g.qoff + int64_t(b) * g.m * g.r, g.m, g.r, 1});
+                p->unit_group_p.push_back(int32_t(gi));
+                p->unit_group_q.push_back(int32_t(gi));
             }
             p->panel_p = std::max(p->panel_p, g.n);  // longest rank>1 panel (rows)
             p->panel_q = std::max(p->panel_q, g.m);
@@ -1042,9 +1106,11 @@ static int decompress_f64(psgd_plan* p, void* const* grads, void* out, int64_t s
 }
 
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
-                         bool fuse, bool write_out, const FlatArgs* fl = nullptr) {
+                         bool fuse, bool write_out, const FlatArgs* fl = nullptr,
+                         const psgd_plan::Span* span = nullptr) {
     if (p->f64()) return compress_f64(p, grads, step, it, s);
     if (int st = refresh_pointers(p, grads, s)) return st;
+    const psgd_plan::Span sp = span ? *span : p->full_span();
     const bool even = p->even(step, it);
     float* in = even ? p->P : p->Q;
     float* out = even ? p->Q : p->P;
@@ -1056,19 +1122,20 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
 
     if (!fused && !fused0) {
         OrthArgs oa{};
-        oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q);
+        const int32_t* ur = even ? sp.up : sp.uq;
+        oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q) + ur[0];
         oa.state = in;
         oa.hx = p->hist(0, it);
         oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
-        const int nunits = int(even ? p->units_p.size() : p->units_q.size());
-        PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+        const int nunits = ur[1] - ur[0];
+        if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
     }
 
     if (it == p->iters - 1 && p->fused_final(step)) {
         // last iteration, odd: product + residual (+ output at world size 1) in one pass
         FinalArgs fa{};
         fa.mats = p->dev<MatDesc>(p->o_mats);
-        fa.tiles = p->dev<Tile>(p->o_tiles_fin);
+        fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
         fa.grads = p->grad_tab.table();
         fa.out = p->out_now;
         fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
@@ -1083,23 +1150,23 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
             fa.xstate = in;
             fa.hx = p->hist(0, it);
         }
-        fa.ntiles = int32_t(p->tiles_fin.size());
+        const int nfin = sp.fin[1] - sp.fin[0];
+        fa.ntiles = nfin;
         if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
+        if (nfin + fa.flat.nitems == 0) return PSGD_OK;
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
         if (int st = timing_begin(p, s, &ev)) return st;
         if (p->fin_lds)
-            PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa,
-                                      int(p->tiles_fin.size()), s));
+            PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa, nfin, s));
         else
-            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa,
-                                      int(p->tiles_fin.size()), s));
+            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa, nfin, s));
         if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
         return PSGD_OK;
     }
 
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
-    pa.tiles = p->dev<Tile>(p->o_tiles);
+    pa.tiles = p->dev<Tile>(p->o_tiles) + sp.tiles[0];
     pa.grads = p->grad_tab.table();
     pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
@@ -1110,31 +1177,34 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
     if (even) {
-        PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, int(p->tiles.size()), s));
+        const int nt = sp.tiles[1] - sp.tiles[0];
+        if (nt > 0) PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, nt, s));
     } else {
-        if (!p->tiles_ov.empty()) {
-            pa.tiles = p->dev<Tile>(p->o_tiles_ov);
-            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, it, pa, int(p->tiles_ov.size()), s));
+        if (sp.ov[1] > sp.ov[0]) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_ov) + sp.ov[0];
+            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, it, pa, sp.ov[1] - sp.ov[0], s));
         }
-        if (!p->tiles_om.empty()) {
-            pa.tiles = p->dev<Tile>(p->o_tiles_om);
-            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), it, pa, int(p->tiles_om.size()), s));
+        if (sp.om[1] > sp.om[0]) {
+            pa.tiles = p->dev<Tile>(p->o_tiles_om) + sp.om[0];
+            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), it, pa, sp.om[1] - sp.om[0], s));
         }
     }
 
     ReduceArgs ra{};
     ra.mats = pa.mats;
-    ra.items = p->dev<RedItem>(even ? p->o_red_even : p->o_red_odd);
+    const int32_t* rr = even ? sp.re : sp.ro;  // this parity's items (out-factor side)
+    const int32_t* rn = even ? sp.ro : sp.re;  // the other parity's items (in-factor side)
+    ra.items = p->dev<RedItem>(even ? p->o_red_even : p->o_red_odd) + rr[0];
     ra.part = pa.part;
     ra.yloc = p->hist(1, it);
     ra.state = out;
     ra.even = even ? 1 : 0;
-    ra.nmain = int(even ? p->red_even.size() : p->red_odd.size());
+    ra.nmain = rr[1] - rr[0];
     if (fused0) {  // normalise the state P in place + history copy (P-side items)
         ra.ss_in = pa.ss0;
         ra.grng_in = p->dev<int32_t>(p->o_grng_ss0);
-        ra.nitems = p->dev<RedItem>(p->o_red_odd);
-        ra.nnorm = int(p->red_odd.size());
+        ra.nitems = p->dev<RedItem>(p->o_red_odd) + sp.ro[0];
+        ra.nnorm = sp.ro[1] - sp.ro[0];
         ra.raw = in;
         ra.xstate = in;
         ra.hx = p->hist(0, it);
@@ -1142,14 +1212,15 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
         ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
         ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
-        ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even);
-        ra.nnorm = int(even ? p->red_odd.size() : p->red_even.size());
+        ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even) + rn[0];
+        ra.nnorm = rn[1] - rn[0];
         ra.raw = p->hist(1, it - 1);
         ra.xstate = in;
         ra.hx = p->hist(0, it);
     }
-    if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters) ra.ss_out = ss + size_t(it & 1) * p->ss_stride;
-    PSGD_HIP(launch_reduce(ra, ra.nmain + ra.nnorm, s));
+    // ss_out is indexed by the launch's block (item) index: offset like the item list
+    if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters) ra.ss_out = ss + size_t(it & 1) * p->ss_stride + rr[0];
+    if (ra.nmain + ra.nnorm > 0) PSGD_HIP(launch_reduce(ra, ra.nmain + ra.nnorm, s));
     return PSGD_OK;
 }
 
@@ -1162,13 +1233,16 @@ int psgd_compress(psgd_plan* p, void* const* grads, int64_t step, int32_t it, vo
 }
 
 static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world,
-                           hipStream_t s, bool fuse, const FlatArgs* fl = nullptr) {
+                           hipStream_t s, bool fuse, const FlatArgs* fl = nullptr,
+                           const psgd_plan::Span* span = nullptr) {
     if (p->f64()) return decompress_f64(p, grads, out, step, world, s);
     if (int st = refresh_pointers(p, grads, s)) return st;
+    const psgd_plan::Span sp = span ? *span : p->full_span();
+    const int nt = sp.tiles[1] - sp.tiles[0];
     const int I = p->iters;
     ApplyArgs aa{};
     aa.mats = p->dev<MatDesc>(p->o_mats);
-    aa.tiles = p->dev<Tile>(p->o_tiles);
+    aa.tiles = p->dev<Tile>(p->o_tiles) + sp.tiles[0];
     aa.grads = p->grad_tab.table();
     aa.out = out;
     fill_terms(p, step, I, aa.res);
@@ -1185,15 +1259,16 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
     if (p->fused_final(step)) {
         // the residual was written by the fused last iteration: output only
-        aa.ntiles = int32_t(p->tiles.size());
-        PSGD_HIP(launch_lowrank_out(p->dtype, p->rbucket, I, aa, int(p->tiles.size()), s));
+        aa.ntiles = nt;
+        if (nt > 0) PSGD_HIP(launch_lowrank_out(p->dtype, p->rbucket, I, aa, nt, s));
         return PSGD_OK;
     }
-    aa.ntiles = int32_t(p->tiles.size());
+    aa.ntiles = nt;
     if (fl) aa.flat = *fl;  // uncompressed tensors ride in the same launch
+    if (nt + aa.flat.nitems == 0) return PSGD_OK;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (int st = timing_begin(p, s, &ev)) return st;
-    PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, int(p->tiles.size()), s));
+    PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, nt, s));
     if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
     return PSGD_OK;
 }
@@ -1206,6 +1281,75 @@ int psgd_decompress(psgd_plan* p, void* const* grads, void* out, int64_t step, i
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     DevScope scope(p->device);
     return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false);
+}
+
+// ------------------------------------------------------------- buckets (W > 1) ---
+int psgd_plan_set_buckets(psgd_plan* p, int32_t nbuckets, const int32_t* group_end) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (nbuckets < 0 || (nbuckets > 0 && !group_end)) return fail(PSGD_ERR_VALUE, "bad bucket list");
+    const int32_t ng = int32_t(p->groups.size());
+    int32_t prev = 0;
+    for (int b = 0; b < nbuckets; ++b) {
+        if (group_end[b] <= prev || group_end[b] > ng) return fail(PSGD_ERR_VALUE, "bucket group ends must increase");
+        prev = group_end[b];
+    }
+    if (nbuckets > 0 && prev != ng) return fail(PSGD_ERR_VALUE, "the last bucket must end at the last group");
+    DevScope scope(p->device);
+    if (p->bound) PSGD_HIP(hipDeviceSynchronize());  // the tile tables are rewritten below
+    p->bucket_gend.assign(group_end, group_end + nbuckets);
+    p->spans.clear();
+    if (!p->f64()) {
+        p->set_vec(p->vec_now);  // matrix-ordered tile lists (PSGD_SORT_TILES is off with buckets)
+        if (p->bound)
+            if (int st = p->upload_tiles()) return st;
+    }
+    if (!p->bucket_gend.empty()) p->build_spans();
+    return PSGD_OK;
+}
+
+int psgd_plan_bucket_range(const psgd_plan* p, int32_t b, int64_t* p_off, int64_t* p_len, int64_t* q_off,
+                           int64_t* q_len) {
+    if (!p || b < 0 || b >= int32_t(std::max<size_t>(p->spans.size(), 1))) return fail(PSGD_ERR_VALUE, "bucket out of range");
+    const psgd_plan::Span sp = p->spans.empty() ? p->full_span() : p->spans[b];
+    if (p_off) *p_off = sp.p[0];
+    if (p_len) *p_len = sp.p[1] - sp.p[0];
+    if (q_off) *q_off = sp.q[0];
+    if (q_len) *q_len = sp.q[1] - sp.q[0];
+    return PSGD_OK;
+}
+
+static int bucket_span(const psgd_plan* p, int32_t b, psgd_plan::Span* sp) {
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "buckets are not supported for fp64 plans");
+    if (p->spans.empty()) {
+        if (b != 0) return fail(PSGD_ERR_VALUE, "bucket out of range");
+        *sp = p->full_span();
+        return PSGD_OK;
+    }
+    if (b < 0 || b >= int32_t(p->spans.size())) return fail(PSGD_ERR_VALUE, "bucket out of range");
+    *sp = p->spans[b];
+    return PSGD_OK;
+}
+
+int psgd_compress_bucket(psgd_plan* p, void* const* grads, int64_t step, int32_t it, int32_t bucket, void* stream) {
+    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
+    psgd_plan::Span sp;
+    if (int st = bucket_span(p, bucket, &sp)) return st;
+    DevScope scope(p->device);
+    return compress_impl(p, grads, step, it, static_cast<hipStream_t>(stream), false, false, nullptr, &sp);
+}
+
+int psgd_decompress_bucket(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t world, int32_t bucket,
+                           void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0 || world < 1) return fail(PSGD_ERR_VALUE, "step/world size out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    psgd_plan::Span sp;
+    if (int st = bucket_span(p, bucket, &sp)) return st;
+    DevScope scope(p->device);
+    return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false, nullptr, &sp);
 }
 
 // ------------------------------------------------- building blocks (reducer variants) ---

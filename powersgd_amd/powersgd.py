@@ -278,6 +278,7 @@ class BasicPowerSGD(Aggregator):
                                           self._code, self._dev_index)
         self._p_comm: Optional[torch.Tensor] = None
         self._q_comm: Optional[torch.Tensor] = None
+        self._buckets: Optional[List[tuple]] = None  # W > 1: (p_off, p_len, q_off, q_len) per bucket
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
@@ -320,19 +321,71 @@ class BasicPowerSGD(Aggregator):
         if is_distributed():
             world = torch.distributed.get_world_size()
             iters = self.config.num_iters_per_step
-            for it in range(iters):
-                self._plan.compress(ptrs, step, it, stream)
-                buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
-                if it == iters - 1 and last_comm is not None:
-                    buf = last_comm
-                torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
-            self._plan.decompress(ptrs, out_ptr, step, world, stream)
+            if self._buckets is None:
+                self._setup_buckets()
+            if len(self._buckets) > 1:
+                self._aggregate_buckets(ptrs, out_ptr, step, world, stream, last_comm)
+            else:
+                for it in range(iters):
+                    self._plan.compress(ptrs, step, it, stream)
+                    buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
+                    if it == iters - 1 and last_comm is not None:
+                        buf = last_comm
+                    torch.distributed.all_reduce(buf)  # SUM of the local factors, reference :207
+                self._plan.decompress(ptrs, out_ptr, step, world, stream)
         elif flat is not None:
             self._plan.aggregate_flat(ptrs, out_ptr, step, flat[0], flat[1], flat[2], stream)
         else:
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
         return outs
+
+    def _setup_buckets(self) -> None:
+        """Cut the shape groups into up to PSGD_BUCKETS (default 4) consecutive buckets of about
+        equal gradient size. Each iteration's factor all-reduce (reference :204-209) is then
+        issued per bucket slice, asynchronously, right after that bucket's kernels: bucket b's
+        collective overlaps bucket b+1's product (RCCL runs on its own stream), and the next
+        iteration of bucket b waits only for bucket b's collective. SUM over slices == SUM over
+        the whole buffer, element by element. fp64 plans and PSGD_BUCKETS=1 keep one collective."""
+        want = int(os.environ.get("PSGD_BUCKETS", "4"))
+        groups = self._plan.groups()
+        if self.dtype == torch.float64 or want <= 1 or len(groups) < 2:
+            self._buckets = [(0, self._ps_buffer.numel(), 0, self._qs_buffer.numel())]
+            return
+        cost = [c * n * m for n, m, _r, c in groups]
+        total, nb = float(sum(cost)), min(want, len(groups))
+        ends, acc = [], 0.0
+        for g, c in enumerate(cost):
+            acc += c
+            left_groups, left_buckets = len(groups) - g - 1, nb - len(ends) - 1
+            if len(ends) < nb - 1 and (acc >= total * (len(ends) + 1) / nb or left_groups == left_buckets):
+                ends.append(g + 1)
+        ends.append(len(groups))
+        self._plan.set_buckets(ends)
+        self._buckets = [self._plan.bucket_range(b) for b in range(len(ends))]
+
+    def _aggregate_buckets(self, ptrs: int, out_ptr: int, step: int, world: int, stream: int,
+                           last_comm: Optional[torch.Tensor]) -> None:
+        iters = self.config.num_iters_per_step
+        nb = len(self._buckets)
+        works: List = [None] * nb
+        for it in range(iters):
+            which = self._plan.out_factor(step, it)
+            state = self._qs_buffer if which == 0 else self._ps_buffer
+            comm = last_comm if (it == iters - 1 and last_comm is not None) else None
+            for b, (po, pl, qo, ql) in enumerate(self._buckets):
+                if works[b] is not None:
+                    works[b].wait()  # this bucket's previous collective (stream-ordered under RCCL)
+                self._plan.compress_bucket(ptrs, step, it, b, stream)
+                off, ln = (qo, ql) if which == 0 else (po, pl)
+                if comm is None:
+                    buf = state[off:off + ln]
+                else:  # [factor | uncompressed tail]: the last bucket's slice carries the tail
+                    buf = comm[off:] if b == nb - 1 else comm[off:off + ln]
+                works[b] = torch.distributed.all_reduce(buf, async_op=True)  # SUM, reference :207
+        for b in range(nb):
+            works[b].wait()
+            self._plan.decompress_bucket(ptrs, out_ptr, step, world, b, stream)
 
     def _init_p_batch(self, shape: torch.Size, params: List[torch.Tensor]) -> torch.Tensor:
         rank = min(self.config.rank, min(shape))

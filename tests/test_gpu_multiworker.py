@@ -57,3 +57,66 @@ def test_multiworker_gloo_on_one_gpu(key):
     with tempfile.TemporaryDirectory() as td:
         torch.multiprocessing.spawn(_worker, args=(world, key, os.path.join(td, "init")), nprocs=world,
                                     join=True)
+
+
+def _bucket_worker(rank_id, world, initfile, cfg, steps):
+    """ResNet-50 shapes at world size `world`: the bucketed, overlapped collectives (default
+    PSGD_BUCKETS = 4, async all-reduce per bucket slice) against the oracle run in the same
+    processes over the same gloo group, and against the single-collective path bitwise."""
+    import os as _os
+
+    from oracle import powersgd_oracle as O
+    from powersgd_amd import Config, PowerSGD
+    from powersgd_amd.workloads import CONFIGS, hash_tensors
+
+    torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id,
+                                         world_size=world)
+    try:
+        c = CONFIGS[cfg]
+        shapes = c["shapes"]
+        dev = torch.device("cuda:0")
+        runs = []
+        for buckets in ("4", "1"):
+            _os.environ["PSGD_BUCKETS"] = buckets
+            psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+            ora = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
+            ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
+            ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+            res_d = [torch.zeros(s, device=dev) for s in shapes]
+            res_c = [torch.zeros(s) for s in shapes]
+            outs_all = []
+            for t in range(steps):
+                new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=500 + 10 * t + rank_id)]
+                gd = [r + x.to(dev) for r, x in zip(res_d, new)]
+                gc = [r + x for r, x in zip(res_c, new)]
+                scale = [g.clone() for g in gc]
+                od = psgd.aggregate(gd)
+                oc = O.policy_step(ora, gc, world, lambda b: torch.distributed.all_reduce(b))
+                torch.cuda.synchronize()
+                for i, g in enumerate(scale):
+                    tol = 1e-5 if t == 0 else TOL_FREE
+                    check(_rel_err(od[i], oc[i], g), tol, cfg, buckets, rank_id, t, i, "out")
+                    check(_rel_err(gd[i], gc[i], g), tol, cfg, buckets, rank_id, t, i, "res")
+                outs_all.append([o.clone() for o in od] + [g.clone() for g in gd])
+                res_d, res_c = gd, gc
+            runs.append((len(psgd._powersgd._buckets), outs_all))
+        assert runs[0][0] > 1 and runs[1][0] == 1, (runs[0][0], runs[1][0])
+        if world == 2:  # a SUM of two values does not depend on the order: bitwise equal
+            for a, b in zip(runs[0][1], runs[1][1]):
+                for x, y in zip(a, b):
+                    assert torch.equal(x, y)
+        torch.distributed.barrier()
+    finally:
+        _os.environ.pop("PSGD_BUCKETS", None)
+        torch.distributed.destroy_process_group()
+
+
+def _rel_err(a, b, scale):
+    return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
+
+
+@pytest.mark.parametrize("cfg,world", [("cfg3_resnet50_r4", 2), ("cfg2_resnet50_r1", 2), ("cfg2_resnet50_r1", 4)])
+def test_bucketed_collectives_vs_oracle(cfg, world):
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_bucket_worker, args=(world, os.path.join(td, "init"), cfg, 2), nprocs=world,
+                                    join=True)
