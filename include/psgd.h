@@ -147,6 +147,20 @@ int psgd_compress_bucket(psgd_plan* plan, void* const* grads, int64_t step, int3
 int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64_t step,
                            int32_t world_size, int32_t bucket, void* stream);
 
+/* ----------------------------- one-shot all-reduce of the last factor over IPC (W > 1) ------ */
+/* Single node, one process per GPU: instead of a ring all-reduce of the last iteration's
+ * out-factor (powersgd.py:204-209), every rank reads all ranks' copies directly through IPC
+ * mappings over xGMI and sums them in rank order. psgd_ipc_create allocates this rank's exchange
+ * buffer and exports its handle (psgd_ipc_handle_bytes bytes); the caller all-gathers the handles
+ * and calls psgd_ipc_open. Per step, after the last psgd_compress: psgd_ipc_publish (local factor
+ * -> exchange buffer), a cross-rank barrier (every rank published; and, before publishing, every
+ * rank finished the previous step's sum), psgd_ipc_sum (state <- SUM), then psgd_decompress. */
+int psgd_ipc_handle_bytes(int64_t* bytes);
+int psgd_ipc_create(psgd_plan* plan, void* handle_out);
+int psgd_ipc_open(psgd_plan* plan, int32_t world_size, int32_t rank, const void* handles);
+int psgd_ipc_publish(psgd_plan* plan, int64_t step, void* stream);
+int psgd_ipc_sum(psgd_plan* plan, int64_t step, void* stream);
+
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);
 

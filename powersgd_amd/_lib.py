@@ -53,6 +53,11 @@ _SIGNATURES = {
     "psgd_plan_bucket_range": ([_vp, _i32, _P_i64, _P_i64, _P_i64, _P_i64], _i32),
     "psgd_compress_bucket": ([_vp, _vp, _i64, _i32, _i32, _vp], _i32),
     "psgd_decompress_bucket": ([_vp, _vp, _vp, _i64, _i32, _i32, _vp], _i32),
+    "psgd_ipc_handle_bytes": ([_P_i64], _i32),
+    "psgd_ipc_create": ([_vp, _vp], _i32),
+    "psgd_ipc_open": ([_vp, _i32, _i32, _vp], _i32),
+    "psgd_ipc_publish": ([_vp, _i64, _vp], _i32),
+    "psgd_ipc_sum": ([_vp, _i64, _vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -199,6 +204,25 @@ class Plan:
 
     def decompress_bucket(self, grads, out_ptr: int, step: int, world: int, bucket: int, stream: int) -> None:
         check(lib().psgd_decompress_bucket(self._h, grads, out_ptr, step, world, bucket, stream))
+
+    # --- one-shot all-reduce of the last factor over IPC mappings (W > 1, one node)
+    def ipc_create(self) -> bytes:
+        n = _i64()
+        check(lib().psgd_ipc_handle_bytes(ctypes.byref(n)))
+        buf = (ctypes.c_uint8 * n.value)()
+        check(lib().psgd_ipc_create(self._h, buf))
+        return bytes(buf)
+
+    def ipc_open(self, world: int, rank: int, handles: Sequence[bytes]) -> None:
+        blob = b"".join(handles)
+        arr = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(lib().psgd_ipc_open(self._h, world, rank, arr))
+
+    def ipc_publish(self, step: int, stream: int) -> None:
+        check(lib().psgd_ipc_publish(self._h, step, stream))
+
+    def ipc_sum(self, step: int, stream: int) -> None:
+        check(lib().psgd_ipc_sum(self._h, step, stream))
 
     def fused_final(self, step: int) -> bool:
         """True when the last iteration of ``step`` runs fused with the final pass."""

@@ -236,4 +236,14 @@ hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
 hipError_t launch_flat_pack_f64(const FlatArgs& a, hipStream_t s);
 
+// one-shot all-reduce over IPC-mapped exchange buffers (psgd_ipc_*)
+constexpr int kMaxRanks = 64;
+struct IpcSumArgs {
+    const float* const* peers;  // device array: world exchange buffers, rank order
+    float* dst;
+    int64_t n;
+    int32_t world;
+};
+hipError_t launch_ipc_sum(const IpcSumArgs& a, hipStream_t s);
+
 }  // namespace psgd

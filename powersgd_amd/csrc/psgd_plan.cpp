@@ -426,12 +426,21 @@ struct psgd_plan {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
+    // one-shot IPC all-reduce of the last factor (psgd_ipc_*): this rank's exchange buffer
+    // (hipMalloc'd so that it can be exported) and the peers' opened mappings
+    float* ipc_buf = nullptr;
+    std::vector<void*> ipc_peer;
+    int ipc_world = 0, ipc_rank = -1;
+    size_t o_ipc_ptrs = 0;
 
     ~psgd_plan() {
         for (auto& e : ev_pool) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
         }
+        for (size_t w = 0; w < ipc_peer.size(); ++w)
+            if (ipc_peer[w] && int(w) != ipc_rank) (void)hipIpcCloseMemHandle(ipc_peer[w]);
+        if (ipc_buf) (void)hipFree(ipc_buf);
     }
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
@@ -885,6 +894,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     }
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
+    p->o_ipc_ptrs = carve(size_t(kMaxRanks) * sizeof(void*));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
@@ -1350,6 +1360,70 @@ int psgd_decompress_bucket(psgd_plan* p, void* const* grads, void* out, int64_t 
     if (int st = bucket_span(p, bucket, &sp)) return st;
     DevScope scope(p->device);
     return decompress_impl(p, grads, out, step, world, static_cast<hipStream_t>(stream), false, nullptr, &sp);
+}
+
+// ------------------------------------------------- one-shot all-reduce over IPC ---
+int psgd_ipc_handle_bytes(int64_t* bytes) {
+    if (!bytes) return fail(PSGD_ERR_VALUE, "null argument");
+    *bytes = int64_t(sizeof(hipIpcMemHandle_t));
+    return PSGD_OK;
+}
+
+int psgd_ipc_create(psgd_plan* p, void* handle_out) {
+    if (!p || !handle_out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "the IPC all-reduce takes fp32/bf16 plans");
+    DevScope scope(p->device);
+    if (!p->ipc_buf) PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->ipc_buf), size_t(std::max<int64_t>(p->fmax, 1)) * 4));
+    PSGD_HIP(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), p->ipc_buf));
+    return PSGD_OK;
+}
+
+int psgd_ipc_open(psgd_plan* p, int32_t world, int32_t rank, const void* handles) {
+    if (!p || !handles) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->ipc_buf) return fail(PSGD_ERR_STATE, "psgd_ipc_create first");
+    if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return fail(PSGD_ERR_VALUE, "bad world/rank");
+    DevScope scope(p->device);
+    const auto* h = static_cast<const hipIpcMemHandle_t*>(handles);
+    p->ipc_peer.assign(size_t(world), nullptr);
+    p->ipc_world = world;
+    p->ipc_rank = rank;
+    for (int w = 0; w < world; ++w) {
+        if (w == rank) {
+            p->ipc_peer[w] = p->ipc_buf;
+            continue;
+        }
+        PSGD_HIP(hipIpcOpenMemHandle(&p->ipc_peer[w], h[w], hipIpcMemLazyEnablePeerAccess));
+    }
+    return upload(p->dev<void>(p->o_ipc_ptrs), p->ipc_peer.data(), size_t(world) * sizeof(void*));
+}
+
+// the last iteration's LOCAL factor (history slot 1) -> this rank's exchange buffer
+int psgd_ipc_publish(psgd_plan* p, int64_t step, void* stream) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+    DevScope scope(p->device);
+    const int last = p->iters - 1;
+    const int64_t n = p->even(step, last) ? p->qtot : p->ptot;
+    PSGD_HIP(hipMemcpyAsync(p->ipc_buf, p->hist(1, last), size_t(n) * 4, hipMemcpyDeviceToDevice,
+                            static_cast<hipStream_t>(stream)));
+    return PSGD_OK;
+}
+
+// the last iteration's out-factor state <- SUM over the ranks' exchange buffers (one-shot)
+int psgd_ipc_sum(psgd_plan* p, int64_t step, void* stream) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+    DevScope scope(p->device);
+    const int last = p->iters - 1;
+    const bool e = p->even(step, last);
+    IpcSumArgs a{};
+    a.peers = p->dev<const float* const>(p->o_ipc_ptrs);
+    a.dst = e ? p->Q : p->P;
+    a.n = e ? p->qtot : p->ptot;
+    a.world = p->ipc_world;
+    PSGD_HIP(launch_ipc_sum(a, static_cast<hipStream_t>(stream)));
+    return PSGD_OK;
 }
 
 // ------------------------------------------------- building blocks (reducer variants) ---

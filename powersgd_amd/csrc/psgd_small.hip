@@ -1598,6 +1598,28 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- one-shot all-reduce
+// SUM over the ranks' exchange buffers, read directly through IPC mappings (each rank reads
+// all W buffers once: the one-shot form of the reference's all_reduce, powersgd.py:204-209).
+// Fixed rank order, so every rank computes bitwise the same sum. Peer reads are system-scope
+// relaxed atomic loads: they bypass the non-coherent caches, whatever a previous step left there.
+__global__ __launch_bounds__(kBlock) void k_ipc_sum(IpcSumArgs a) {
+    const int64_t stride = int64_t(gridDim.x) * kBlock;
+    for (int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x; e < a.n; e += stride) {
+        float s = __hip_atomic_load(a.peers[0] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int w = 1; w < a.world; ++w)
+            s += __hip_atomic_load(a.peers[w] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        a.dst[e] = s;
+    }
+}
+
+hipError_t launch_ipc_sum(const IpcSumArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
+    k_ipc_sum<<<int(blocks < 1024 ? blocks : 1024), kBlock, 0, s>>>(a);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- flat pack
 // reference powersgd.py:22-31 + utils.py:6-10, :43-49: flat = x / W (division, as div_),
 // then x = 0. One read + two writes per element.

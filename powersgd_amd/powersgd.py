@@ -161,7 +161,8 @@ class PowerSGD(Aggregator):
         unc_shapes = [t.shape for t, c in zip(params, self.is_compressed_mask) if not c]
         self._unc = _FlatEntry(unc_shapes, p._code, p.dtype, p.device) if unc_shapes else None
         # one fp32 collective can carry factor + uncompressed values (fp32 gradients only)
-        self._merge_ok = p.dtype == torch.float32 and os.environ.get("PSGD_MERGE_ALLREDUCE", "1") != "0"
+        self._merge_ok = (p.dtype == torch.float32 and os.environ.get("PSGD_MERGE_ALLREDUCE", "1") != "0"
+                          and os.environ.get("PSGD_IPC_ALLREDUCE") != "1")
         # _merge order: position of tensor i in (compressed outputs + uncompressed outputs)
         nc = sum(self.is_compressed_mask)
         ic, iu, self._order = 0, nc, []
@@ -279,6 +280,7 @@ class BasicPowerSGD(Aggregator):
         self._p_comm: Optional[torch.Tensor] = None
         self._q_comm: Optional[torch.Tensor] = None
         self._buckets: Optional[List[tuple]] = None  # W > 1: (p_off, p_len, q_off, q_len) per bucket
+        self._ipc_open = False  # W > 1 with PSGD_IPC_ALLREDUCE=1: peers' exchange buffers mapped
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
@@ -321,6 +323,10 @@ class BasicPowerSGD(Aggregator):
         if is_distributed():
             world = torch.distributed.get_world_size()
             iters = self.config.num_iters_per_step
+            if os.environ.get("PSGD_IPC_ALLREDUCE") == "1" and last_comm is None and self.dtype != torch.float64:
+                self._aggregate_ipc(ptrs, out_ptr, step, world, stream)
+                self.step_counter += 1
+                return outs
             if self._buckets is None:
                 self._setup_buckets()
             if len(self._buckets) > 1:
@@ -339,6 +345,33 @@ class BasicPowerSGD(Aggregator):
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
         return outs
+
+    def _aggregate_ipc(self, ptrs: int, out_ptr: int, step: int, world: int, stream: int) -> None:
+        """Prototype: the LAST iteration's factor all-reduce as a one-shot sum over IPC mappings
+        (each rank reads every rank's local factor directly, psgd_ipc_*), the earlier iterations
+        as the reference's all_reduce. The two host barriers per step order the exchange buffers
+        across processes; on one node they would become device-side flags."""
+        dist = torch.distributed
+        if not self._ipc_open:
+            handle = self._plan.ipc_create()
+            handles: List = [None] * world
+            dist.all_gather_object(handles, handle)
+            self._plan.ipc_open(world, dist.get_rank(), handles)
+            self._ipc_open = True
+        iters = self.config.num_iters_per_step
+        for it in range(iters):
+            self._plan.compress(ptrs, step, it, stream)
+            if it < iters - 1:
+                buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
+                dist.all_reduce(buf)  # SUM of the local factors, reference :207
+        cur = torch.cuda.current_stream(self.device)
+        cur.synchronize()
+        dist.barrier()  # every rank has finished reading the exchange buffers of the previous step
+        self._plan.ipc_publish(step, stream)
+        cur.synchronize()
+        dist.barrier()  # every rank's local factor is in its exchange buffer
+        self._plan.ipc_sum(step, stream)  # one-shot SUM over the ranks (reference :207)
+        self._plan.decompress(ptrs, out_ptr, step, world, stream)
 
     def _setup_buckets(self) -> None:
         """Cut the shape groups into up to PSGD_BUCKETS (default 4) consecutive buckets of about
