@@ -432,8 +432,30 @@ struct psgd_plan {
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
     size_t o_ipc_ptrs = 0;
+    // World-size-1 steps as HIP graphs (psgd_plan_set_graphs): one captured graph per distinct
+    // (pointer-table slots, output pointers, parity class), replayed with one launch; the buckets
+    // (when set and overlap is on) run on two side streams forked inside the graph.
+    struct GraphEntry {
+        uint64_t key[6];
+        hipGraphExec_t exec;
+        uint64_t stamp;
+    };
+    bool use_graphs = false, overlap = false;  // both opt-in: slower on ROCm 7.2
+    std::vector<GraphEntry> graphs;
+    uint64_t graph_clock = 0;
+    hipStream_t gstream = nullptr, side[2] = {nullptr, nullptr};
+    hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+    void drop_graphs() {
+        for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
+        graphs.clear();
+    }
 
     ~psgd_plan() {
+        drop_graphs();
+        for (hipStream_t st : {gstream, side[0], side[1]})
+            if (st) (void)hipStreamDestroy(st);
+        for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_join[0], ev_join[1]})
+            if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_pool) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -476,6 +498,7 @@ struct psgd_plan {
     bool even(int64_t step, int it) const { return ((step * iters + it) % 2) == 0; }
 
     void set_vec(const std::vector<int>& vec) {
+        drop_graphs();  // captured launch grids / tile lists may change
         vec_now = vec;
         tiles.clear();
         tiles_ov.clear();
@@ -978,6 +1001,7 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     p->P = static_cast<float*>(P);  // fp64 plans: double buffers (see P64/Q64)
     p->Q = static_cast<float*>(Q);
     p->ws = static_cast<char*>(workspace);
+    p->drop_graphs();
     const size_t nt = p->shapes.size();
     p->grad_tab.bind(p->dev<char>(p->o_ptrs), nt);
     p->rdst_tab.bind(p->dev<char>(p->o_rdst), nt);
@@ -1306,6 +1330,7 @@ int psgd_plan_set_buckets(psgd_plan* p, int32_t nbuckets, const int32_t* group_e
     if (nbuckets > 0 && prev != ng) return fail(PSGD_ERR_VALUE, "the last bucket must end at the last group");
     DevScope scope(p->device);
     if (p->bound) PSGD_HIP(hipDeviceSynchronize());  // the tile tables are rewritten below
+    p->drop_graphs();
     p->bucket_gend.assign(group_end, group_end + nbuckets);
     p->spans.clear();
     if (!p->f64()) {
@@ -1578,14 +1603,19 @@ int psgd_plan_timing_read(psgd_plan* p, double* total_ms, int32_t* launches) {
     return PSGD_OK;
 }
 
+static int bucket_span(const psgd_plan* p, int32_t b, psgd_plan::Span* sp);
+static int aggregate_entry(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
+                           const FlatArgs* fl, const psgd_flat* f);
+static int flat_args(psgd_flat* f, void* const* tensors, void* flat, int32_t world, hipStream_t s, FlatArgs* out);
+
 static int aggregate_impl(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
-                          const FlatArgs* fl) {
+                          const FlatArgs* fl, const psgd_plan::Span* span = nullptr) {
     static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;
     p->out_now = out;
     for (int it = 0; it < p->iters; ++it)
-        if (int st = compress_impl(p, grads, step, it, s, fuse, true, fl)) return st;
+        if (int st = compress_impl(p, grads, step, it, s, fuse, true, fl, span)) return st;
     if (p->fused_final(step)) return PSGD_OK;  // output written by the fused last iteration
-    return decompress_impl(p, grads, out, step, 1, s, fuse, fl);
+    return decompress_impl(p, grads, out, step, 1, s, fuse, fl, span);
 }
 
 int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, void* stream) {
@@ -1594,7 +1624,7 @@ int psgd_aggregate(psgd_plan* p, void* const* grads, void* out, int64_t step, vo
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     DevScope scope(p->device);
-    return aggregate_impl(p, grads, out, step, static_cast<hipStream_t>(stream), nullptr);
+    return aggregate_entry(p, grads, out, step, static_cast<hipStream_t>(stream), nullptr, nullptr);
 }
 
 // ------------------------------------------------------------------ flat pack ------
@@ -1677,6 +1707,124 @@ int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world
     return PSGD_OK;
 }
 
+// One world-size-1 step: all buckets at once, or (overlap) bucket b on side stream b % 2,
+// forked from and joined back into `s` with events (legal inside a stream capture).
+static int run_step(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s, const FlatArgs* fl) {
+    if (!p->overlap || p->spans.size() < 2) return aggregate_impl(p, grads, out, step, s, fl);
+    for (int i = 0; i < 2; ++i)
+        if (!p->side[i]) PSGD_HIP(hipStreamCreateWithFlags(&p->side[i], hipStreamNonBlocking));
+    if (!p->ev_fork) {
+        PSGD_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) PSGD_HIP(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
+    }
+    PSGD_HIP(hipEventRecord(p->ev_fork, s));
+    for (int i = 0; i < 2; ++i) PSGD_HIP(hipStreamWaitEvent(p->side[i], p->ev_fork, 0));
+    for (size_t b = 0; b < p->spans.size(); ++b)
+        if (int st = aggregate_impl(p, grads, out, step, p->side[b % 2], b == 0 ? fl : nullptr, &p->spans[b])) return st;
+    for (int i = 0; i < 2; ++i) {
+        PSGD_HIP(hipEventRecord(p->ev_join[i], p->side[i]));
+        PSGD_HIP(hipStreamWaitEvent(s, p->ev_join[i], 0));
+    }
+    return PSGD_OK;
+}
+
+// World-size-1 entry (psgd_aggregate / psgd_aggregate_flat): the pointer tables are selected
+// (or uploaded) on the caller's stream first, then the step runs as a replayed HIP graph keyed
+// by everything its launches bake in, on the plan's own stream between two events (the caller's
+// stream may be the legacy default stream, which cannot be captured).
+static int aggregate_entry(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
+                           const FlatArgs* fl, const psgd_flat* f) {
+    // the pointer tables are selected (uploaded) on the caller's stream before any fork or capture:
+    // the side streams and the graph then only ever hit
+    if (int st = refresh_pointers(p, grads, s)) return st;
+    const bool graph = p->use_graphs && !p->timing && !p->f64();
+    if (!graph) return run_step(p, grads, out, step, s, fl);
+    const uint64_t key[6] = {uint64_t(p->grad_tab.cur), uint64_t(reinterpret_cast<uintptr_t>(out)),
+                             uint64_t(reinterpret_cast<uintptr_t>(fl ? fl->flat : nullptr)),
+                             uint64_t(fl && f ? f->tab.cur : -1), uint64_t((step * p->iters) & 1),
+                             uint64_t(p->overlap ? 1 : 0)};
+    if (!p->gstream) {
+        PSGD_HIP(hipStreamCreateWithFlags(&p->gstream, hipStreamNonBlocking));
+        PSGD_HIP(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+        PSGD_HIP(hipEventCreateWithFlags(&p->ev_out, hipEventDisableTiming));
+    }
+    psgd_plan::GraphEntry* ge = nullptr;
+    for (auto& g : p->graphs)
+        if (std::equal(key, key + 6, g.key)) ge = &g;
+    if (!ge) {
+        if (p->graphs.size() >= 16) {  // least recently used goes
+            auto lru = std::min_element(p->graphs.begin(), p->graphs.end(),
+                                        [](const auto& a, const auto& b) { return a.stamp < b.stamp; });
+            (void)hipGraphExecDestroy(lru->exec);
+            p->graphs.erase(lru);
+        }
+        hipGraph_t g = nullptr;
+        PSGD_HIP(hipStreamBeginCapture(p->gstream, hipStreamCaptureModeThreadLocal));
+        const int st = run_step(p, grads, out, step, p->gstream, fl);
+        const hipError_t e = hipStreamEndCapture(p->gstream, &g);
+        if (st) {
+            if (g) (void)hipGraphDestroy(g);
+            return st;
+        }
+        if (e != hipSuccess) return fail(PSGD_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        psgd_plan::GraphEntry ne{};
+        std::copy(key, key + 6, ne.key);
+        const hipError_t ie = hipGraphInstantiate(&ne.exec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ie != hipSuccess) return fail(PSGD_ERR_DEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        p->graphs.push_back(ne);
+        ge = &p->graphs.back();
+    }
+    ge->stamp = ++p->graph_clock;
+    PSGD_HIP(hipEventRecord(p->ev_in, s));
+    PSGD_HIP(hipStreamWaitEvent(p->gstream, p->ev_in, 0));
+    PSGD_HIP(hipGraphLaunch(ge->exec, p->gstream));
+    PSGD_HIP(hipEventRecord(p->ev_out, p->gstream));
+    PSGD_HIP(hipStreamWaitEvent(s, p->ev_out, 0));
+    return PSGD_OK;
+}
+
+int psgd_plan_set_graphs(psgd_plan* p, int32_t graphs, int32_t overlap) {
+    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
+    DevScope scope(p->device);
+    if (p->bound && !p->graphs.empty()) PSGD_HIP(hipDeviceSynchronize());
+    p->drop_graphs();
+    p->use_graphs = graphs != 0;
+    p->overlap = overlap != 0;
+    return PSGD_OK;
+}
+
+int psgd_plan_prepare(psgd_plan* p, void* const* grads, void* stream) {
+    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    DevScope scope(p->device);
+    return refresh_pointers(p, grads, static_cast<hipStream_t>(stream));
+}
+
+int psgd_aggregate_bucket(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t bucket, psgd_flat* f,
+                          void* const* unc, void* flat_out, void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    psgd_plan::Span sp;
+    if (int st = bucket_span(p, bucket, &sp)) return st;
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (f && f->total > 0) {
+        if (!unc || !flat_out) return fail(PSGD_ERR_VALUE, "null argument");
+        if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
+        if (f->dtype != p->dtype || f->device != p->device) {
+            if (int st = aggregate_impl(p, grads, out, step, s, nullptr, &sp)) return st;
+            return psgd_flat_pack(f, unc, flat_out, 1, stream);
+        }
+        FlatArgs a;
+        if (int st = flat_args(f, unc, flat_out, 1, s, &a)) return st;
+        return aggregate_impl(p, grads, out, step, s, &a, &sp);
+    }
+    return aggregate_impl(p, grads, out, step, s, nullptr, &sp);
+}
+
 int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f,
                         void* const* unc, void* flat_out, void* stream) {
     if (!f || f->total == 0) return psgd_aggregate(p, grads, out, step, stream);
@@ -1692,7 +1840,7 @@ int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t ste
     hipStream_t s = static_cast<hipStream_t>(stream);
     FlatArgs a;
     if (int st = flat_args(f, unc, flat_out, 1, s, &a)) return st;
-    return aggregate_impl(p, grads, out, step, s, &a);
+    return aggregate_entry(p, grads, out, step, s, &a, f);
 }
 
 }  // extern "C"

@@ -250,3 +250,31 @@ def test_wide_rank_free_running(rank, iters):
             check(_rel(od[i], oc[i], g), TOL_FREE, rank, iters, t, i, "out")
             check(_rel(gd[i], gc[i], g), TOL_FREE, rank, iters, t, i, "res")
         res_d, res_c = gd, gc
+
+
+@pytest.mark.parametrize("rank,iters,dtype", [(1, 2, torch.float32), (4, 2, torch.float32), (2, 1, torch.float32),
+                                             (2, 3, torch.bfloat16)])
+def test_w1_bucket_overlap_bitwise(rank, iters, dtype):
+    """World size 1, ResNet-50 shapes: the buckets run as independent sub-steps on two side
+    streams inside the step's HIP graph (psgd_plan_set_graphs). Same tiles, same reduction
+    order: the result must be bitwise the one of the single-stream launch sequence, over
+    several steps (alternating parities at I = 1 and 3)."""
+    shapes = resnet50_shapes()
+    runs = []
+    for overlap in (True, False):
+        psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dtype) for s in shapes], Config(rank, 2, iters, 0))
+        psgd._powersgd._graphs = overlap  # the opt-in graph + side-stream mode against plain launches
+        psgd._powersgd.overlap = overlap
+        res = [torch.zeros(s, device=DEV, dtype=dtype) for s in shapes]
+        got = []
+        for t in range(3):
+            grads = [(r + torch.from_numpy(f).to(DEV)).to(dtype) for r, f in zip(res, hash_tensors(shapes, seed=40 + t))]
+            outs = psgd.aggregate(grads)
+            torch.cuda.synchronize()
+            got.append([o.clone() for o in outs] + [g.clone() for g in grads])
+            res = grads
+        assert psgd._powersgd.overlap == overlap
+        runs.append(got)
+    for a, b in zip(runs[0], runs[1]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
