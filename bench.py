@@ -245,6 +245,7 @@ def main():
     def kernel_pass(pick):
         # the kernels alone: at world size 1 the bucket overlap (two side streams) would make
         # the event-bracketed durations of concurrent launches overlap, so it is off here
+        was = codec._overlap_on
         codec.overlap = False
         codec._plan.set_timing(True)
         first = codec.step_counter
@@ -253,7 +254,7 @@ def main():
         torch.cuda.synchronize()
         total_ms, launches = codec._plan.timing_read()
         codec._plan.set_timing(False)
-        codec.overlap = True
+        codec.overlap = was
         return total_ms / max(launches, 1), first
 
     apply_ms_cold, first_cold = kernel_pass(lambda k: k % S) if do_cold else (None, None)

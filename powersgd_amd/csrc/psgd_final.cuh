@@ -285,6 +285,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     // segments past S load zeros (kOob) and drop their stores; their arithmetic is skipped
     // by a uniform branch
     auto seg_on = [&](int s) { return s < S; };
+    float ssq = 0.f;  // product-only: sum of squares of this thread's P rows (row-group leaders)
     auto process = [&](Batch& bt, int b) {
         const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
         int64_t ic[RB];
@@ -373,9 +374,11 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             const int64_t e = d.poff + (ib + u) * r + c;
                             a.yloc[e] = dot[u][c];
                             a.state[e] = dot[u][c];
+                            ssq = fmaf(dot[u][c], dot[u][c], ssq);
                         }
                 }
         }
+        if (a.product_only) return;  // a later iteration forms residual and output
         // residual (and output at world size 1) from the registers
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -437,12 +440,25 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         load(ga, b + 2);
         if (b + 1 < nb) process(gb, b + 1);
     }
+    if (a.product_only && a.ss_out) {
+        // this row block's sum of squares of P: row-group leaders in row-group order (fixed)
+        __syncthreads();  // the last batch's row sums may still be read from `red`
+        if (tt == 0) red[rg] = ssq;
+        __syncthreads();
+        if (tid == 0) {
+            float tot = 0.f;
+            for (int g2 = 0; g2 < RGS; ++g2) tot += red[g2];
+            a.ss_out[blockIdx.x - a.flat.nitems] = tot;
+        }
+    }
 }
 
 template <typename T, int R, int K, int SMAX>
 __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
     constexpr int NT = FinNT<R>::value, RB = FinRB<R>::value;
-    __shared__ float red[2 * (NT / 64) * RB * R];
+    // batch row sums (2 buffers) and, in product-only mode, one sum of squares per row group
+    constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
+    __shared__ float red[kRed];
     // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
     // not in the launch tail); then the row blocks
     const int nf = a.flat.nitems;
@@ -464,7 +480,8 @@ constexpr int kFinLdsNT = 1024;
 template <typename T, int R, int K, int SMAX>
 __global__ __launch_bounds__(kFinLdsNT) void k_final_lds(FinalArgs a) {
     constexpr int NT = kFinLdsNT, RB = 1;
-    __shared__ float red[2 * (NT / 64) * RB * R];
+    constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
+    __shared__ float red[kRed];
     extern __shared__ __attribute__((aligned(16))) float pan[];
     const int nf = a.flat.nitems;
     if (int(blockIdx.x) < nf) {

@@ -166,6 +166,11 @@ struct FinalArgs {
     float* hx;
     int32_t ntiles;       // row blocks; flat pack items come first (as ApplyArgs)
     FlatArgs flat;
+    // product only (an odd iteration that is NOT the last one, world size 1): P rows are
+    // written (yloc/state) but neither the residual nor the output; each row block writes the
+    // sum of squares of its P rows to ss_out[block] (the next iteration's rank-1 joint norm)
+    int32_t product_only;
+    float* ss_out;
 };
 
 struct OrthArgs {

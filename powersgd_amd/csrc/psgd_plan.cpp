@@ -329,6 +329,11 @@ struct psgd_plan {
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
     std::vector<Tile> tiles_fin; // row blocks of the fused final odd pass
     bool fin_ok = false;         // every matrix fits the fused final odd pass
+    // per group [begin, end) of its row blocks in tiles_fin (for the product-only form's
+    // per-block sums of squares); false when the blocks of a group are not contiguous
+    std::vector<int32_t> grng_fin;
+    bool fin_grng_ok = false;
+    size_t o_grng_fin = 0, o_ss_fin = 0;
     bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
     int fin_smax = 0;
     int fin_lds_bytes = 0;
@@ -621,10 +626,29 @@ struct psgd_plan {
             std::stable_sort(tiles.begin(), tiles.end(), by(cost_col));
             std::stable_sort(tiles_ov.begin(), tiles_ov.end(), by(cost_col));
         }
+        grng_fin.assign(2 * groups.size(), 0);
+        fin_grng_ok = fin_ok;
+        for (size_t g = 0; g < groups.size() && fin_grng_ok; ++g) {
+            int32_t b = -1, e = -1;
+            for (size_t i = 0; i < tiles_fin.size(); ++i)
+                if (mats[tiles_fin[i].mat].group == int32_t(g)) {
+                    if (b < 0) b = int32_t(i);
+                    else if (e != int32_t(i)) fin_grng_ok = false;  // not contiguous
+                    e = int32_t(i) + 1;
+                }
+            grng_fin[2 * g] = b < 0 ? 0 : b;
+            grng_fin[2 * g + 1] = e < 0 ? 0 : e;
+        }
         if (!bucket_gend.empty()) build_spans();
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits)
     bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
+    // an odd iteration before the last one, at world size 1 (fuse): P in the row-resident final
+    // kernel in product-only form (no partials, no reduction launch)
+    bool fin_prod(int64_t step, int it, bool fuse) const {
+        return fuse && fin_ok && fin_grng_ok && it < iters - 1 && !even(step, it) &&
+               env_int("PSGD_FIN_PRODUCT", 0) != 0;  // opt-in: neutral-to-slower on cfg5
+    }
     bool fused_final_at(int64_t step, int it) const { return it == iters - 1 && fused_final(step); }
 
     int upload_tiles() const;
@@ -681,6 +705,7 @@ int psgd_plan::upload_tiles() const {
     if (int st = upload(dev<void>(o_tiles), tiles.data(), tiles.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_fin), tiles_fin.data(), tiles_fin.size() * sizeof(Tile))) return st;
+    if (int st = upload(dev<void>(o_grng_fin), grng_fin.data(), grng_fin.size() * sizeof(int32_t))) return st;
     return upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile));
 }
 
@@ -924,6 +949,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
     p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
     p->o_ss = carve(2 * p->ss_stride * sizeof(float));
+    p->o_grng_fin = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->o_ss_fin = carve(2 * size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(float));
     p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float));
     p->o_ss0_base = carve(std::max<size_t>(p->ss0_base.size(), 1) * sizeof(int32_t));
     p->o_grng_ss0 = carve(std::max<size_t>(p->grng_ss0.size(), 1) * sizeof(int32_t));
@@ -1165,8 +1192,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
     }
 
-    if (it == p->iters - 1 && p->fused_final(step)) {
-        // last iteration, odd: product + residual (+ output at world size 1) in one pass
+    const bool fprod = p->fin_prod(step, it, fuse);
+    const bool prev_fprod = it > 0 && p->fin_prod(step, it - 1, fuse);
+    const int64_t fin_stride = std::max<int64_t>(p->tiles_fin_cap, 1);
+    if ((it == p->iters - 1 && p->fused_final(step)) || fprod) {
+        // last iteration, odd: product + residual (+ output at world size 1) in one pass;
+        // fprod: an earlier odd iteration, product only
         FinalArgs fa{};
         fa.mats = p->dev<MatDesc>(p->o_mats);
         fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
@@ -1175,7 +1206,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
         fill_terms(p, step, it, fa.res);
         fa.nres = it;
-        fa.write_out = write_out ? 1 : 0;
+        fa.write_out = (write_out && !fprod) ? 1 : 0;
+        fa.product_only = fprod ? 1 : 0;
+        if (fprod && fused_norm(p, fuse, it + 1))
+            fa.ss_out = p->dev<float>(p->o_ss_fin) + size_t(it & 1) * fin_stride + sp.fin[0];
         fa.yloc = p->hist(1, it);
         fa.state = out;
         if (fused) {
@@ -1186,10 +1220,11 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         }
         const int nfin = sp.fin[1] - sp.fin[0];
         fa.ntiles = nfin;
-        if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
+        if (fl && write_out && !fprod) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         if (nfin + fa.flat.nitems == 0) return PSGD_OK;
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-        if (int st = timing_begin(p, s, &ev)) return st;
+        if (!fprod)  // benchmark timing covers the final pass only
+            if (int st = timing_begin(p, s, &ev)) return st;
         if (p->fin_lds)
             PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa, nfin, s));
         else
@@ -1246,6 +1281,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
         ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
         ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
+        if (prev_fprod) {  // the in-factor came from a product-only final: per-row-block sums
+            ra.ss_in = p->dev<float>(p->o_ss_fin) + size_t((it - 1) & 1) * fin_stride;
+            ra.grng_in = p->dev<int32_t>(p->o_grng_fin);
+        }
         ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even) + rn[0];
         ra.nnorm = rn[1] - rn[0];
         ra.raw = p->hist(1, it - 1);

@@ -1563,12 +1563,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         ssv = gb + lane < ge ? a.ss_in[gb + lane] : 0.f;
     }
     float s = 0.f;
-    for (int c = c0; c < c1; c += 8) {  // loads issued 8 at a time (clamped, unconditional)
-        float v[8];
+    // loads issued kRedBatch at a time (clamped, unconditional): the partials were just written
+    // on other XCDs, so each batch is one MALL round trip; small plans have up to 256 partials
+    // per element (64 per wave), which 8-deep batches turned into 8 serial round trips
+    constexpr int kRedBatch = 16;
+    for (int c = c0; c < c1; c += kRedBatch) {
+        float v[kRedBatch];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
+        for (int q = 0; q < kRedBatch; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < kRedBatch; ++q) {
             keep(v[q]);
             s += c + q < c1 ? v[q] : 0.f;
         }
