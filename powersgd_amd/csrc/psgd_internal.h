@@ -37,6 +37,19 @@ struct MatDesc {
     int32_t fin_S;
     int32_t fin_rows;
     int32_t fin_pad;
+    // even product with the reduction folded in: this matrix's column strips own the ticket /
+    // sum-of-squares slots [slot0, slot0 + nstrip)
+    int32_t slot0;
+    int32_t pad2;
+};
+
+// One shape group, for the folded even reduction (joint norm, in-factor normalisation).
+struct GroupDesc {
+    int64_t poff, qoff;  // factor offsets of the group's first matrix
+    int64_t n, m;
+    int32_t r, count;
+    int32_t strips;      // strip slots of the group (sum over its matrices)
+    int32_t slot0;       // first strip slot of the group
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
@@ -100,6 +113,24 @@ struct ProductArgs {
     // tiles write sum_rows P^2 of their row chunk to ss0[ss0_base[mat] + chunk]
     float* ss0;
     const int32_t* ss0_base;
+    // Even products with the partial reduction FOLDED IN (no k_reduce launch): the last tile
+    // of each column strip to finish (agent-scope release + ticket) sums the strip's partials,
+    // divides by the in-factor's joint norm (norm 1: from ss_in over grng_in; norm 2: of raw_in
+    // over the group) and writes yloc/state (+ the strip's sum of squares to ss_out); the last
+    // strip of a group then writes the normalised in-factor (raw_in / norm) to xstate and hx.
+    int32_t fold;
+    int32_t norm;
+    int32_t* cnt;
+    int32_t* gcnt;
+    const GroupDesc* groups;
+    float* yloc;
+    float* state;
+    float* ss_out;
+    const float* ss_in;
+    const int32_t* grng_in;
+    const float* raw_in;
+    float* xstate;
+    float* hx;
 };
 
 struct ApplyArgs {

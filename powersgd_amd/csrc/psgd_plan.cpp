@@ -334,6 +334,13 @@ struct psgd_plan {
     std::vector<int32_t> grng_fin;
     bool fin_grng_ok = false;
     size_t o_grng_fin = 0, o_ss_fin = 0;
+    // even products with the reduction folded in (ProductArgs::fold): strip slots per matrix
+    // (MatDesc::slot0), group descriptors, per-group [begin, end) of strip slots
+    bool fold = false;
+    std::vector<GroupDesc> gdesc;
+    std::vector<int32_t> grng_strip;
+    int64_t slots_cap = 0;
+    size_t o_cnt = 0, o_gcnt = 0, o_ss_strip = 0, o_grng_strip = 0, o_gdesc = 0;
     bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
     int fin_smax = 0;
     int fin_lds_bytes = 0;
@@ -550,6 +557,25 @@ struct psgd_plan {
                 d.odd_nstrip = g.nstrip;
             }
         }
+        // strip slots of the folded even reduction (matrix order; a group's slots contiguous)
+        gdesc.assign(groups.size(), GroupDesc{});
+        grng_strip.assign(2 * groups.size(), 0);
+        {
+            int32_t slot = 0;
+            for (size_t i = 0; i < mats.size(); ++i) {
+                MatDesc& d = mats[i];
+                GroupDesc& gd = gdesc[d.group];
+                if (i == 0 || mats[i - 1].group != d.group) {
+                    const auto& gr = groups[d.group];
+                    gd = GroupDesc{gr.poff, gr.qoff, gr.n, gr.m, gr.r, int32_t(gr.tensors.size()), 0, slot};
+                    grng_strip[2 * d.group] = slot;
+                }
+                d.slot0 = slot;
+                slot += d.nstrip;
+                gd.strips += d.nstrip;
+                grng_strip[2 * d.group + 1] = slot;
+            }
+        }
         fin_ok = false;
         fin_lds = false;
         // buffer descriptors address one matrix: keep each below 2^31 bytes
@@ -706,6 +732,8 @@ int psgd_plan::upload_tiles() const {
     if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_fin), tiles_fin.data(), tiles_fin.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_grng_fin), grng_fin.data(), grng_fin.size() * sizeof(int32_t))) return st;
+    if (int st = upload(dev<void>(o_gdesc), gdesc.data(), gdesc.size() * sizeof(GroupDesc))) return st;
+    if (int st = upload(dev<void>(o_grng_strip), grng_strip.data(), grng_strip.size() * sizeof(int32_t))) return st;
     return upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile));
 }
 
@@ -887,6 +915,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         md.part_odd = p->part_floats;
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
+        p->slots_cap += std::max(a.nstrip, b.nstrip);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
         int64_t cap = fin_geometry(md.n, md.m, fin_form(p->rbucket, true), p->fin_elems_lds).ntiles;
         for (int sc = 0; sc <= 5; ++sc)  // any segment cap set_vec may pick
@@ -950,6 +979,11 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
     p->o_ss = carve(2 * p->ss_stride * sizeof(float));
     p->o_grng_fin = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->o_cnt = carve(size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(int32_t));
+    p->o_gcnt = carve(std::max<size_t>(p->groups.size(), 1) * sizeof(int32_t));
+    p->o_ss_strip = carve(2 * size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(float));
+    p->o_grng_strip = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->o_gdesc = carve(std::max<size_t>(p->groups.size(), 1) * sizeof(GroupDesc));
     p->o_ss_fin = carve(2 * size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(float));
     p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float));
     p->o_ss0_base = carve(std::max<size_t>(p->ss0_base.size(), 1) * sizeof(int32_t));
@@ -1045,6 +1079,12 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     if (int st = upload(p->dev<void>(p->o_ss0_base), p->ss0_base.data(), p->ss0_base.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_ss0), p->grng_ss0.data(), p->grng_ss0.size() * sizeof(int32_t))) return st;
     PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float)));
+    // tickets of the folded reduction start at zero (each last arriver resets its own)
+    PSGD_HIP(hipMemset(p->dev<void>(p->o_cnt), 0, size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(int32_t)));
+    PSGD_HIP(hipMemset(p->dev<void>(p->o_gcnt), 0, std::max<size_t>(p->groups.size(), 1) * sizeof(int32_t)));
+    // opt-in: the in-launch seam measured slower than the k_reduce boundary it replaces on
+    // every BASELINE config (profiles/r02/fold_ab.txt; cdna_hip_programming.md §5.6 agrees)
+    p->fold = env_int("PSGD_FOLD", 0) != 0;
     if (p->f64()) {
         if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
         if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
@@ -1195,6 +1235,18 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     const bool fprod = p->fin_prod(step, it, fuse);
     const bool prev_fprod = it > 0 && p->fin_prod(step, it - 1, fuse);
     const int64_t fin_stride = std::max<int64_t>(p->tiles_fin_cap, 1);
+    const int64_t slot_stride = std::max<int64_t>(p->slots_cap, 1);
+    // even iterations fold their partial reduction into the product (no k_reduce launch)
+    const bool fold = p->fold && even;
+    const bool prev_fold = it > 0 && p->fold && p->even(step, it - 1);
+    // where the previous iteration's reduction left the per-slot sums of squares of its
+    // out-factor (this iteration's raw in-factor) and the per-group slot ranges
+    const float* prev_ss = prev_fold    ? p->dev<float>(p->o_ss_strip) + size_t((it - 1) & 1) * slot_stride
+                           : prev_fprod ? p->dev<float>(p->o_ss_fin) + size_t((it - 1) & 1) * fin_stride
+                                        : ss + size_t((it - 1) & 1) * p->ss_stride;
+    const int32_t* prev_grng = prev_fold    ? p->dev<int32_t>(p->o_grng_strip)
+                               : prev_fprod ? p->dev<int32_t>(p->o_grng_fin)
+                                            : p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
     if ((it == p->iters - 1 && p->fused_final(step)) || fprod) {
         // last iteration, odd: product + residual (+ output at world size 1) in one pass;
         // fprod: an earlier odd iteration, product only
@@ -1213,8 +1265,8 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         fa.yloc = p->hist(1, it);
         fa.state = out;
         if (fused) {
-            fa.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
-            fa.grng_in = p->dev<int32_t>(p->o_grng_even);  // in-factor Q came from an even reduce
+            fa.ss_in = prev_ss;  // the in-factor Q came from an even iteration's reduction
+            fa.grng_in = prev_grng;
             fa.xstate = in;
             fa.hx = p->hist(0, it);
         }
@@ -1239,15 +1291,39 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     pa.grads = p->grad_tab.table();
     pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
-    if (fused0) {
+    if (fused0 && !fold) {
         pa.ss0 = p->dev<float>(p->o_ss0);
         pa.ss0_base = p->dev<int32_t>(p->o_ss0_base);
+    }
+    if (fold) {
+        pa.fold = 1;
+        pa.cnt = p->dev<int32_t>(p->o_cnt);
+        pa.gcnt = p->dev<int32_t>(p->o_gcnt);
+        pa.groups = p->dev<GroupDesc>(p->o_gdesc);
+        pa.yloc = p->hist(1, it);
+        pa.state = out;
+        if (fused0) {  // the raw state P's joint norm; the group's last strip normalises P
+            pa.norm = 2;
+            pa.raw_in = in;
+            pa.xstate = in;
+            pa.hx = p->hist(0, it);
+        } else if (fused) {
+            pa.norm = 1;
+            pa.ss_in = prev_ss;
+            pa.grng_in = prev_grng;
+            pa.raw_in = p->hist(1, it - 1);
+            pa.xstate = in;
+            pa.hx = p->hist(0, it);
+        }
+        if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters)
+            pa.ss_out = p->dev<float>(p->o_ss_strip) + size_t(it & 1) * slot_stride;
     }
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
     if (even) {
         const int nt = sp.tiles[1] - sp.tiles[0];
         if (nt > 0) PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, nt, s));
+        if (fold) return PSGD_OK;  // the last tile of each strip reduced it
     } else {
         if (sp.ov[1] > sp.ov[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov) + sp.ov[0];
@@ -1279,12 +1355,8 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         ra.hx = p->hist(0, it);
     }
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
-        ra.ss_in = ss + size_t((it - 1) & 1) * p->ss_stride;
-        ra.grng_in = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
-        if (prev_fprod) {  // the in-factor came from a product-only final: per-row-block sums
-            ra.ss_in = p->dev<float>(p->o_ss_fin) + size_t((it - 1) & 1) * fin_stride;
-            ra.grng_in = p->dev<int32_t>(p->o_grng_fin);
-        }
+        ra.ss_in = prev_ss;
+        ra.grng_in = prev_grng;
         ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even) + rn[0];
         ra.nnorm = rn[1] - rn[0];
         ra.raw = p->hist(1, it - 1);

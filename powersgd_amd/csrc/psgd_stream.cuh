@@ -641,7 +641,128 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
             for (int w = 1; w < kWaves; ++w) s += lds[w * width + idx];
             const int c = idx % R;
             const int64_t col = int64_t(t.strip) * g.L * V + idx / R;
-            if (c < r && col < g.m) part[col * r + c] = s;
+            // write-through (sc1) stores: the folded reduction's last arriver on another XCD
+            // reads them after an acquire, with no release fence (and its L2 write-back) here
+            if (c < r && col < g.m)
+                __hip_atomic_store(&part[col * r + c], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ------------------------------------------------ folded even reduction (epilogue) --
+// Publish this workgroup's stores and take a ticket on `cnt` (cdna_hip_programming.md §5
+// "In-launch split-K reduction": the partial slabs are written through (sc1), so every wave's
+// vmcnt drain + the relaxed agent-scope fetch_add suffice; `release` adds the agent-scope
+// release for plain stores. The last arriver resets the counter for the next launch and
+// acquires before it reads the other workgroups' data). True in the last arriving workgroup.
+__device__ __forceinline__ bool arrive_last(int32_t* cnt, int32_t target, float* lds, bool release) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (release) {  // plain stores to publish; write-through (sc1) stores need no fence
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const int32_t old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = old == target - 1;
+        if (last) {
+            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds[0] = last ? 1.f : 0.f;
+    }
+    __syncthreads();
+    const bool last = lds[0] != 0.f;
+    __syncthreads();  // lds[0] is scratch again
+    return last;
+}
+
+// The last tile of a column strip: sum the strip's partials over the row chunks (fixed order),
+// divide by the in-factor's joint norm, write the out-factor (history + state) and the strip's
+// sum of squares; the last strip of the group writes the normalised in-factor.
+__device__ __forceinline__ void fold_even_strip(const ProductArgs& a, const MatDesc& d, const Tile& t, float* lds) {
+    if (!arrive_last(a.cnt + d.slot0 + t.strip, d.nchunk, lds, false)) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = d.r;
+    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+    const int64_t c0 = int64_t(t.strip) * W, c1 = d.m < c0 + W ? d.m : c0 + W;
+    const int64_t e0 = c0 * r, e1 = c1 * r, len = d.m * r;
+    const GroupDesc g = a.groups[d.group];
+    float dn = 1.f;
+    if (a.norm == 1) {
+        dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
+    } else if (a.norm == 2) {  // the raw in-factor's joint norm (orthogonalization.py:5-6)
+        // every wave of every reducer of the group: the same lane-strided order, 16 loads in
+        // flight per lane (a dependent chain of single loads cost one MALL round trip each)
+        const int64_t gl = int64_t(g.count) * g.n * g.r;
+        const float* x0 = a.raw_in + g.poff;
+        float acc = 0.f;
+        for (int64_t e0 = lane; e0 < gl; e0 += 64 * 16) {
+            float v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int64_t e = e0 + int64_t(q) * 64;
+                v[q] = x0[e < gl ? e : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                keep(v[q]);
+                const float x = e0 + int64_t(q) * 64 < gl ? v[q] : 0.f;
+                acc = fmaf(x, x, acc);
+            }
+        }
+        const float nrm = sqrtf(wave_allsum(acc));
+        dn = nrm > 1e-16f ? nrm : 1e-16f;
+    }
+    const float* part = a.part + d.part_even;
+    constexpr int kB = 16;
+    float ssq = 0.f;
+    for (int64_t e = e0 + tid; e < e1; e += kBlock) {
+        float sum = 0.f;
+        for (int c = 0; c < d.nchunk; c += kB) {  // kB loads in flight (clamped, unconditional)
+            float v[kB];
+#pragma unroll
+            for (int q = 0; q < kB; ++q) v[q] = part[int64_t(c + q < d.nchunk ? c + q : 0) * len + e];
+#pragma unroll
+            for (int q = 0; q < kB; ++q) {
+                keep(v[q]);
+                sum += c + q < d.nchunk ? v[q] : 0.f;
+            }
+        }
+        if (a.norm) sum = sum / dn;  // G^T (x / d) == (G^T x) / d up to rounding
+        a.yloc[d.qoff + e] = sum;
+        a.state[d.qoff + e] = sum;
+        ssq = fmaf(sum, sum, ssq);
+    }
+    if (a.ss_out) {
+        ssq = wave_allsum(ssq);
+        if (lane == 0) lds[1 + wave] = ssq;
+        __syncthreads();
+        if (tid == 0) a.ss_out[d.slot0 + t.strip] = ((lds[1] + lds[2]) + lds[3]) + lds[4];
+    }
+    if (!a.xstate) return;
+    // group ticket: orders the other strips' reads of the raw in-factor before the overwrite
+    if (!arrive_last(a.gcnt + d.group, g.strips, lds, true)) return;
+    // the whole group's strips are reduced (so all of its product tiles are done): the
+    // in-factor may be overwritten with its normalised values (matrix.div_, :6)
+    const int64_t gl = int64_t(g.count) * g.n * g.r;
+    for (int64_t e0 = tid; e0 < gl; e0 += int64_t(kBlock) * 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int64_t e = e0 + int64_t(q) * kBlock;
+            v[q] = a.raw_in[g.poff + (e < gl ? e : 0)];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            keep(v[q]);
+            const int64_t e = e0 + int64_t(q) * kBlock;
+            if (e < gl) {
+                const float x = v[q] / dn;
+                a.xstate[g.poff + e] = x;
+                a.hx[g.poff + e] = x;
+            }
         }
     }
 }
@@ -661,10 +782,16 @@ __global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
     if constexpr (R <= 8) {
         if (d.vec) {
             product_tile<T, R, K, EVEN, 4>(a, d, t, lds);
+            if constexpr (EVEN) {
+                if (a.fold) fold_even_strip(a, d, t, lds);
+            }
             return;
         }
     }
     product_tile<T, R, K, EVEN, 1>(a, d, t, lds);
+    if constexpr (EVEN) {
+        if (a.fold) fold_even_strip(a, d, t, lds);
+    }
 }
 
 // ------------------------------------------------------- odd product on MFMA -------
