@@ -266,7 +266,7 @@ hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArg
                             hipStream_t s, int* waves = nullptr);
 hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
-hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, hipStream_t s);
+hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, bool chol, hipStream_t s);
 // paper-code Gram-Schmidt (gradient_reducers.py:945-956) on one panel per unit, per matrix
 hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);

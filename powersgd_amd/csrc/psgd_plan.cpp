@@ -337,6 +337,7 @@ struct psgd_plan {
     // even products with the reduction folded in (ProductArgs::fold): strip slots per matrix
     // (MatDesc::slot0), group descriptors, per-group [begin, end) of strip slots
     bool fold = false;
+    bool orth_chol = true;  // PSGD_ORTH_CHOL, read at bind (Cholesky-QR vs Householder)
     std::vector<GroupDesc> gdesc;
     std::vector<int32_t> grng_strip;
     int64_t slots_cap = 0;
@@ -1085,6 +1086,7 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     // opt-in: the in-launch seam measured slower than the k_reduce boundary it replaces on
     // every BASELINE config (profiles/r02/fold_ab.txt; cdna_hip_programming.md §5.6 agrees)
     p->fold = env_int("PSGD_FOLD", 0) != 0;
+    p->orth_chol = env_int("PSGD_ORTH_CHOL", 1) != 0;
     if (p->f64()) {
         if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
         if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
@@ -1229,7 +1231,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         oa.hx = p->hist(0, it);
         oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
         const int nunits = ur[1] - ur[0];
-        if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, s));
+        if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, p->orth_chol, s));
     }
 
     const bool fprod = p->fin_prod(step, it, fuse);
@@ -1630,7 +1632,7 @@ int psgd_orthogonalize(psgd_plan* p, int32_t which, float* buf, int32_t mode, vo
     } else {
         oa.units = p->dev<OrthUnit>(which ? p->o_units_p : p->o_units_q);
         const int nunits = int(which ? p->units_p.size() : p->units_q.size());
-        PSGD_HIP(launch_orth(oa, nunits, p->rbucket, which ? p->panel_p : p->panel_q, s));
+        PSGD_HIP(launch_orth(oa, nunits, p->rbucket, which ? p->panel_p : p->panel_q, p->orth_chol, s));
     }
     return PSGD_OK;
 }

@@ -28,13 +28,16 @@ __device__ unsigned long long g_stamps[64];
 #endif
 
 // Sum NV floats over a workgroup of NW waves; result in every thread. `red` holds
-// 2 * NW * NV floats (double-buffered by `phase`, so one barrier per call suffices).
-template <int NV, int NW>
+// 2 * NW * SLOT floats (double-buffered by `phase`, so one barrier per call suffices).
+// SLOT is the largest NV the kernel sums: the two buffers sit at fixed offsets, so calls
+// of different widths never overlap the buffer the previous call is still being read from.
+template <int NV, int NW, int SLOT>
 __device__ __forceinline__ void wg_sum(float (&v)[NV], float* red, int& phase) {
+    static_assert(NV <= SLOT, "wg_sum: NV exceeds the buffer slot");
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = wave_allsum(v[i]);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float* buf = red + phase * NW * NV;
+    float* buf = red + phase * NW * SLOT;
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) buf[wave * NV + i] = v[i];
@@ -292,7 +295,8 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, double* rd
 // LAPACK geqr2 + org2r as 3r - 1 workgroup reductions.
 template <int R, int RPT>
 __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
-    __shared__ __attribute__((aligned(16))) float red[2 * kOrthWaves * (R > 2 ? R : 2)];
+    constexpr int kSlot = R > 2 ? R : 2;  // widest wg_sum below
+    __shared__ __attribute__((aligned(16))) float red[2 * kOrthWaves * kSlot];
     const OrthUnit u = a.units[blockIdx.x];
     if (u.r == 1) {
         orth_joint_norm(a, u, reinterpret_cast<double*>(red));
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
                 if (i > j && i < k) v2[0] = fmaf(x, x, v2[0]);
                 if (i == j) v2[1] = x;
             }
-            wg_sum<2, kOrthWaves>(v2, red, phase);
+            wg_sum<2, kOrthWaves, kSlot>(v2, red, phase);
             PSGD_STAMP(3 + 2 * j);
             const float alpha = v2[1];
             float tj = 0.f;
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
 #pragma unroll
                     for (int c = j + 1; c < R; ++c) w[c] = fmaf(vi, A[q][c], w[c]);
                 }
-                wg_sum<R, kOrthWaves>(w, red, phase);
+                wg_sum<R, kOrthWaves, kSlot>(w, red, phase);
 #pragma unroll
                 for (int q = 0; q < RPT; ++q) {
                     const int64_t i = tid + int64_t(q) * kOrthThreads;
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
 #pragma unroll
                     for (int c = j + 1; c < R; ++c) w[c] = fmaf(vi, A[q][c], w[c]);
                 }
-                wg_sum<R, kOrthWaves>(w, red, phase);
+                wg_sum<R, kOrthWaves, kSlot>(w, red, phase);
 #pragma unroll
                 for (int q = 0; q < RPT; ++q) {
                     const int64_t i = tid + int64_t(q) * kOrthThreads;
@@ -451,13 +455,14 @@ __global__ __launch_bounds__(kOrthThreads) void k_orth_reg(OrthArgs a) {
 // no barriers); NW = 4/8/16 -> the whole workgroup of 64*NW threads works on one panel
 // (rows tid + 64*NW*q, cross-wave sums through LDS). More waves per panel means fewer rows
 // per wave and several waves per SIMD to hide each other's latency.
-template <int NV, int NW>
+template <int NV, int NW, int SLOT>
 __device__ __forceinline__ void grp_sum(float (&v)[NV], float* red, int& phase) {
+    static_assert(NV <= SLOT, "grp_sum: NV exceeds the buffer slot");
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = wave_allsum(v[i]);
     if constexpr (NW > 1) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        float* buf = red + phase * (NW + 1) * NV;
+        float* buf = red + phase * (NW + 1) * SLOT;
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < NV; ++i) buf[wave * NV + i] = v[i];
@@ -508,7 +513,7 @@ __device__ void joint_norm_grp(const OrthArgs& a, const OrthUnit& u, float* red)
         }
     }
     int phase = 0;
-    grp_sum<1, NW>(part, red, phase);
+    grp_sum<1, NW, 1>(part, red, phase);
     const float nrm = sqrtf(part[0]);
     const float d = nrm > 1e-16f ? nrm : 1e-16f;  // torch.maximum(norm, eps)
     for (int64_t base = t; base < total; base += int64_t(U) * NT) {
@@ -635,7 +640,7 @@ __global__ __launch_bounds__(NW == 1 ? kBlock : 64 * NW) void k_orth_wy(OrthArgs
                 for (int c = j + 1; c < R; ++c) v[2 + c] = fmaf(x, A[q][c], v[2 + c]);
             }
         }
-        grp_sum<2 + 2 * R, NW>(v, red, phase);
+        grp_sum<2 + 2 * R, NW, kRed>(v, red, phase);
         const float alpha = v[1];
         if (v[0] != 0.f) {  // LAPACK slarfg: xnorm == 0 -> tau = 0, H_j = I
             const float beta = -copysignf(hypotf(alpha, sqrtf(v[0])), alpha);
@@ -690,7 +695,7 @@ __global__ __launch_bounds__(NW == 1 ? kBlock : 64 * NW) void k_orth_wy(OrthArgs
                 for (int b = a2 + 1; b < R; ++b) sv2[a2 * R + b] = fmaf(A[q][a2], A[q][b], sv2[a2 * R + b]);
         }
     }
-    grp_sum<2 * R * R, NW>(sv2, red, phase);
+    grp_sum<2 * R * R, NW, kRed>(sv2, red, phase);
     float T[R][R];
 #pragma unroll
     for (int a2 = 0; a2 < R; ++a2)
@@ -922,6 +927,10 @@ __device__ __forceinline__ void block_sum_f64(double (&v)[NV], double* red) {
 
 // NT threads per panel: 512 for r <= 4 (a 4096-row panel is one batch of loads per pass;
 // the kernel is latency-bound, one workgroup per panel), 256 for r = 8 (registers).
+// A sign pivot |T_jj| within this of 1 marks a column LAPACK leaves unreflected (tau = 0)
+// or nearly so; orthonormal-column entries of a real panel sit far below it.
+constexpr double kSignTol = 1e-5;
+
 template <int R>
 struct CholNT {
     static constexpr int value = R <= 4 ? 512 : 256;
@@ -1052,6 +1061,10 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
         for (int j = 0; j < R; ++j) {
             if (j < r) {
                 const bool nonneg = T[j][j] >= 0.0;
+                // |T_jj| = 1 is LAPACK's xnorm == 0 column (tau = 0, beta = alpha, no flip):
+                // the reconstruction cannot tell it from a tiny trailing sub-column, so such
+                // panels (e.g. upper trapezoidal) take the exact Householder recursion
+                ok = ok && !(j < k - 1 && fabs(T[j][j]) > 1.0 - kSignTol);
                 sgn[j] = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
                 T[j][j] -= sgn[j];
 #pragma unroll
@@ -1307,6 +1320,7 @@ __device__ __forceinline__ void orth_chol_wide(const OrthArgs& a) {
             lds_fence();
             const double tjj = tsh[j * R + j];
             const bool nonneg = tjj >= 0.0;
+            ok = ok && !(j < k - 1 && fabs(tjj) > 1.0 - kSignTol);  // see orth_chol_panel
             const double sj = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
             if (lane == j) sg = sj;
             const double piv = tjj - sj;
@@ -1484,15 +1498,11 @@ hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
+hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, bool chol, hipStream_t s) {
     // register-resident path when the longest rank>1 panel fits RPT * R <= 128 floats/thread
     int64_t rpt = 1;
     while (rpt * kOrthThreads < kmax) rpt <<= 1;
     if (R == 1) return launch_orth_reg_r<1>(1, a, nunits, s);
-    static const bool chol = [] {
-        const char* e = std::getenv("PSGD_ORTH_CHOL");
-        return !e || std::atoi(e) != 0;
-    }();
     static const int diag = [] {
         const char* e = std::getenv("PSGD_ORTH_DIAG");
         return e ? std::atoi(e) : 0;

@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from oracle import powersgd_oracle as O
+from parity_log import check
 from powersgd_amd import Config, PowerSGD
 from powersgd_amd.workloads import hash_tensors
 
@@ -37,7 +38,51 @@ def test_state_signs_match_lapack(rank, chol):
         O.policy_step(ora, [x.clone() for x in g])
         torch.cuda.synchronize()
         p_gpu = psgd._powersgd._ps_buffer.cpu()
-        assert float((p_gpu - ora.codec.p_flat).abs().max()) <= 1e-5
+        check(float((p_gpu - ora.codec.p_flat).abs().max()), 1e-5, "orth_state", rank, chol)
+    finally:
+        if old is None:
+            os.environ.pop("PSGD_ORTH_CHOL", None)
+        else:
+            os.environ["PSGD_ORTH_CHOL"] = old
+
+
+def _structure_(view, kind, rank):
+    """Give every P panel [B, n, r] a column LAPACK leaves unreflected (zero trailing
+    sub-column: xnorm == 0, tau = 0, beta = alpha, so no sign flip)."""
+    r = view.shape[2]
+    if kind == "trapezoid":  # upper trapezoidal, mixed-sign diagonal: every column
+        view[:, r:, :] = 0.0
+        view.copy_(torch.triu(view))
+        sign = torch.tensor([(-1.0) ** (j + rank) for j in range(r)])
+        view.copy_(view.abs() * torch.where(torch.eye(view.shape[1], r) > 0, sign, torch.ones(r)))
+    else:  # only column 0 = -2 e_0; the others stay random
+        view[:, :, 0] = 0.0
+        view[:, 0, 0] = -2.0
+
+
+@pytest.mark.parametrize("rank", [2, 3, 4, 8, 16, 32])
+@pytest.mark.parametrize("kind", ["trapezoid", "col0"])
+@pytest.mark.parametrize("chol", ["1", "0"])
+def test_unreflected_columns_match_lapack(rank, kind, chol):
+    """the Cholesky-QR sign reconstruction assumed beta = -sign(alpha) for
+    every column but the last; a zero trailing sub-column (tau = 0) must keep LAPACK's
+    sign. Such panels are routed to the Householder recursion (k_orth_chol ok = false)."""
+    old = os.environ.get("PSGD_ORTH_CHOL")
+    os.environ["PSGD_ORTH_CHOL"] = chol
+    try:
+        psgd = PowerSGD([torch.zeros(s, device=DEV) for s in SHAPES], Config(rank, 0.1, 1, 0))
+        ora = O.policy_init([torch.zeros(s) for s in SHAPES], rank, 0.1, 1, 0)
+        for v in ora.codec.p_views:
+            _structure_(v, kind, rank)
+        psgd._powersgd._ps_buffer.copy_(ora.codec.p_flat.to(DEV))
+        ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+        g = [torch.from_numpy(f) for f in hash_tensors(SHAPES, seed=29)]
+        psgd.aggregate([x.to(DEV) for x in g])
+        O.policy_step(ora, [x.clone() for x in g])
+        torch.cuda.synchronize()
+        p_gpu = psgd._powersgd._ps_buffer.cpu()
+        err = float((p_gpu - ora.codec.p_flat).abs().max())
+        check(err, 1e-5, "orth_unreflected", kind, rank, chol)
     finally:
         if old is None:
             os.environ.pop("PSGD_ORTH_CHOL", None)

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 20; ++rep) {
         (void)hipMemcpy(st, h.data(), h.size() * 4, hipMemcpyHostToDevice);
         (void)hipEventRecord(e0, 0);
-        (void)launch_orth(a, nunits, r, k, 0);
+        (void)launch_orth(a, nunits, r, k, false, 0);
         (void)hipEventRecord(e1, 0);
         (void)hipEventSynchronize(e1);
         float ms;
