@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2_resnet50_r1", choices=sorted(CONFIGS))
     ap.add_argument("--sets", type=int, default=4, help="gradient sets rotated in the cold loop")
+    ap.add_argument("--iters", type=int, default=None,
+                    help="experiments only: override the config's num_iters_per_step (reported in config)")
     ap.add_argument("--mode", default="both", choices=["both", "cold", "warm"],
                     help="profiling runs: time only one cache state (the headline needs 'both' or 'cold')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -220,6 +222,8 @@ def main():
     dev = torch.device("cuda", local)
     c = dict(CONFIGS[a.config])
     c["name"] = a.config
+    if a.iters is not None:
+        c["iters"] = a.iters
     dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
     shapes = c["shapes"]
     S = max(1, a.sets)
@@ -267,7 +271,7 @@ def main():
     mask = psgd.is_compressed_mask
     # which final pass each timed step took (I odd: steps alternate between the fused last odd
     # iteration and k_apply); bytes are averaged over the timed steps
-    nf = sum(codec._plan.fused_final(t) for t in range(first_cold, first_cold + a.steps))
+    nf = sum(codec._plan.fused_final(t, world == 1) for t in range(first_cold, first_cold + a.steps))
     frac_f = nf / a.steps
     ab = frac_f * apply_alg_bytes(c, mask, world, True) + (1 - frac_f) * apply_alg_bytes(c, mask, world, False)
     sb = frac_f * step_alg_bytes(c, mask, world, True) + (1 - frac_f) * step_alg_bytes(c, mask, world, False)

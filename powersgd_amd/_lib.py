@@ -37,7 +37,7 @@ _SIGNATURES = {
     "psgd_compress": ([_vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_decompress": ([_vp, _vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_aggregate": ([_vp, _vp, _vp, _i64, _vp], _i32),
-    "psgd_plan_fused_final": ([_vp, _i64, _P_i32], _i32),
+    "psgd_plan_fused_final": ([_vp, _i64, _i32, _P_i32], _i32),
     "psgd_plan_set_timing": ([_vp, _i32], _i32),
     "psgd_plan_timing_read": ([_vp, _P_dbl, _P_i32], _i32),
     "psgd_flat_create": ([_P_i64, _i32, _i32, ctypes.POINTER(_vp)], _i32),
@@ -238,10 +238,11 @@ class Plan:
     def ipc_sum(self, step: int, stream: int) -> None:
         check(lib().psgd_ipc_sum(self._h, step, stream))
 
-    def fused_final(self, step: int) -> bool:
-        """True when the last iteration of ``step`` runs fused with the final pass."""
+    def fused_final(self, step: int, aggregate: bool = True) -> bool:
+        """True when the last iteration of ``step`` runs fused with the final pass
+        (``aggregate``: in ``psgd_aggregate``, the world-size-1 path; else the building blocks)."""
         f = _i32()
-        check(lib().psgd_plan_fused_final(self._h, step, ctypes.byref(f)))
+        check(lib().psgd_plan_fused_final(self._h, step, 1 if aggregate else 0, ctypes.byref(f)))
         return bool(f.value)
 
     # --- building blocks (paper-code reducer variants, powersgd_amd/reducers.py)

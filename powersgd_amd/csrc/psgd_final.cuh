@@ -108,9 +108,15 @@ __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c
 // PL (panels in LDS): the factor panels X and Q_0 of the whole matrix live in LDS (`pan`,
 // [m][R] each, R floats per column) instead of per-thread registers, so a rank-4 row needs no
 // register panels and a 1024-thread workgroup keeps 16 waves of rows in flight.
-template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PL>
+// PJ (projection form, two power iterations at world size 1, K = 0): X = orth(Q_0) with
+// Q_0 = X R' (R' = the QR factor the orthonormalisation left in a.proj_r), so the reference's
+// output P_0 Q_0^T + P_1 X^T with P_1 = (G - P_0 Q_0^T) X is exactly G X X^T and the residual
+// G - G X X^T (reference powersgd.py:185-230 with I = 2): the row pass needs X alone, no error
+// feedback term per element. The P state the reference keeps is P_1 = G X - P_0 R'^T (X^T X
+// = I), formed per row from the row sum.
+template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PL, bool PJ = false>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
-                                               float* red, float* pan) {
+                                               float* red, float* pan, float* rqs = nullptr) {
     constexpr int KC = K > 0 ? K : 1;
     constexpr int NW = NT / 64;
     const int r = d.r;
@@ -146,6 +152,15 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         const int32_t c = (s * Tg + tt) * 4;
         act[s] = s < S && c < m;
         ccol[s] = act[s] ? c : 0;
+    }
+    // PJ: R' of this matrix (r x r, row-major at its Q-layout offset; zero outside r x r),
+    // staged in LDS: only the row-group leaders read it, once per row (no registers held)
+    if constexpr (PJ) {
+        if (tid < R * R) {
+            const int c = tid / R, l = tid - (tid / R) * R;
+            rqs[tid] = (c < r && l < r) ? a.proj_r[d.qoff + c * r + l] : 0.f;
+        }
+        __syncthreads();
     }
     // factor row of column c (clamped to column 0 past the end of a ragged row)
     auto fcol = [&](int s, int v) { return ccol[s] + v < m ? ccol[s] + v : 0; };
@@ -368,13 +383,22 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
             for (int u = 0; u < RB; ++u)
                 if (ib + u < row_end) {
+                    float p0[PJ ? R : 1];  // PJ: this row of P_0 (leaders only, loaded here)
+                    if constexpr (PJ) ld_factor<R>(gconst<float>(a.proj_p0) + d.poff + (ib + u) * r, r, p0);
 #pragma unroll
                     for (int c = 0; c < R; ++c)
                         if (c < r) {
                             const int64_t e = d.poff + (ib + u) * r + c;
-                            a.yloc[e] = dot[u][c];
-                            a.state[e] = dot[u][c];
-                            ssq = fmaf(dot[u][c], dot[u][c], ssq);
+                            float y = dot[u][c];
+                            if constexpr (PJ) {  // P_1 = G X - P_0 R'^T
+                                float t = 0.f;
+#pragma unroll
+                                for (int l = 0; l < R; ++l) t = fmaf(p0[l], rqs[c * R + l], t);
+                                y = y - t;
+                            }
+                            a.yloc[e] = y;
+                            a.state[e] = y;
+                            ssq = fmaf(y, y, ssq);
                         }
                 }
         }
@@ -453,12 +477,13 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     }
 }
 
-template <typename T, int R, int K, int SMAX>
-__global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
+template <typename T, int R, int K, int SMAX, bool PJ = false>
+__device__ __forceinline__ void final_odd_block(const FinalArgs& a) {
     constexpr int NT = FinNT<R>::value, RB = FinRB<R>::value;
     // batch row sums (2 buffers) and, in product-only mode, one sum of squares per row group
     constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
     __shared__ float red[kRed];
+    __shared__ float rqs[PJ ? R * R : 1];
     // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
     // not in the launch tail); then the row blocks
     const int nf = a.flat.nitems;
@@ -469,9 +494,22 @@ __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
     const Tile t = a.tiles[blockIdx.x - nf];
     const MatDesc d = a.mats[t.mat];
     if (d.vec)
-        final_odd_tile<T, R, K, SMAX, true, NT, RB, false>(a, d, t, red, nullptr);
+        final_odd_tile<T, R, K, SMAX, true, NT, RB, false, PJ>(a, d, t, red, nullptr, rqs);
     else
-        final_odd_tile<T, R, K, SMAX, false, NT, RB, false>(a, d, t, red, nullptr);
+        final_odd_tile<T, R, K, SMAX, false, NT, RB, false, PJ>(a, d, t, red, nullptr, rqs);
+}
+
+template <typename T, int R, int K, int SMAX>
+__global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
+    final_odd_block<T, R, K, SMAX, false>(a);
+}
+
+// Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
+// CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
+template <typename T, int R, int SMAX>
+__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : 1))) void k_final_proj(
+    FinalArgs a) {
+    final_odd_block<T, R, 0, SMAX, true>(a);
 }
 
 // LDS-panel variant: 1024 threads (16 waves), one workgroup per CU (the panels take up to
@@ -555,11 +593,15 @@ __global__ __launch_bounds__(kBlock) void k_lowrank_out(ApplyArgs a) {
 // SMAX (register segments) is the smallest instantiated bucket >= the plan's max fin_S.
 // ntiles == 0: no launch; `*waves` (if non-null) receives the resident waves per SIMD of
 // the instance that would run (the plan only fuses at >= 2).
-template <typename T, int R, int SMAX, int K>
+template <typename T, int R, int SMAX, int K, bool PJ = false>
 hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     constexpr int NT = FinNT<R>::value;
     if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
-        const void* fn = reinterpret_cast<const void*>(&k_final_odd<T, R, K, SMAX>);
+        const void* fn;
+        if constexpr (PJ)
+            fn = reinterpret_cast<const void*>(&k_final_proj<T, R, SMAX>);
+        else
+            fn = reinterpret_cast<const void*>(&k_final_odd<T, R, K, SMAX>);
         int blocks = 0;
         hipFuncAttributes fa{};
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, NT, 0);
@@ -568,7 +610,10 @@ hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* wa
         *waves = fa.localSizeBytes > 0 ? 0 : blocks * (NT / 64) / 4;
     }
     if (ntiles == 0) return hipSuccess;
-    k_final_odd<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
+    if constexpr (PJ)
+        k_final_proj<T, R, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
+    else
+        k_final_odd<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
     return hipGetLastError();
 }
 
@@ -578,6 +623,9 @@ hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* wa
 // the instance that would run (the plan only fuses at >= 2).
 template <typename T, int R, int SMAX>
 hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    if constexpr (R == 2 || R == 4) {
+        if (nres == kFinProj) return launch_final_k<T, R, SMAX, 0, true>(a, ntiles, s, waves);
+    }
     switch (nres) {
         case 0: return launch_final_k<T, R, SMAX, 0>(a, ntiles, s, waves);
         case 1: return launch_final_k<T, R, SMAX, 1>(a, ntiles, s, waves);

@@ -202,7 +202,12 @@ struct FinalArgs {
     // sum of squares of its P rows to ss_out[block] (the next iteration's rank-1 joint norm)
     int32_t product_only;
     float* ss_out;
+    // projection form (nres = kFinProj, see psgd_final.cuh): P_0 rows and R' per matrix
+    const float* proj_p0;  // P layout
+    const float* proj_r;   // Q layout: R' (r x r, row-major) at each matrix's qoff
 };
+// nres value selecting the projection form of the fused final pass (I = 2, world size 1)
+constexpr int kFinProj = 1000;
 
 struct OrthArgs {
     const OrthUnit* units;
@@ -210,6 +215,10 @@ struct OrthArgs {
     float* hx;           // history copy of the orthonormal in-factor
     float* save;         // if non-null: copy of the pre-orthonormalisation values
     int32_t flags;       // diagnostics (PSGD_ORTH_DIAG): 1 = skip the Householder fallback
+    // if non-null (Cholesky-QR kernels k_orth_chol<R>): the QR factor R' of each panel,
+    // input panel = orthonormal output x R' (upper triangular r x r, row-major, written at the
+    // unit's offset; rank-1 units: the joint-norm divisor at every panel's offset)
+    float* rfac;
 };
 
 // ------------------------------------------------------------------ fp64 gradients

@@ -343,6 +343,7 @@ struct psgd_plan {
     int64_t slots_cap = 0;
     size_t o_cnt = 0, o_gcnt = 0, o_ss_strip = 0, o_grng_strip = 0, o_gdesc = 0;
     bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
+    bool fin_proj = false;       // ... in its projection form (I = 2, psgd_aggregate only)
     int fin_smax = 0;
     int fin_lds_bytes = 0;
     int64_t fin_elems = 32768, fin_elems_lds = 65536, tiles_fin_cap = 0;
@@ -445,6 +446,7 @@ struct psgd_plan {
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
     size_t o_ipc_ptrs = 0;
+    size_t o_rq = 0;  // R' of the last iteration's in-factor panels (projection form), Q layout
     // World-size-1 steps as HIP graphs (psgd_plan_set_graphs): one captured graph per distinct
     // (pointer-table slots, output pointers, parity class), replayed with one launch; the buckets
     // (when set and overlap is on) run on two side streams forked inside the graph.
@@ -579,6 +581,8 @@ struct psgd_plan {
         }
         fin_ok = false;
         fin_lds = false;
+        fin_proj = false;
+        orth_chol = env_int("PSGD_ORTH_CHOL", 1) != 0;
         // buffer descriptors address one matrix: keep each below 2^31 bytes
         bool small = true;
         int64_t mmax = 0;
@@ -611,8 +615,23 @@ struct psgd_plan {
             if (fuse_mode != 3 && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2))) fin_ok = try_form(false);
             if (!fin_ok && fuse_mode == 3 && (rbucket == 2 || rbucket == 4)) fin_ok = fin_lds = try_form(true);
         }
+        // Projection form (psgd_final.cuh): two power iterations at world size 1, ranks 2 and 4,
+        // the last iteration's in-factor orthonormalised by Cholesky-QR (which leaves R').
+        // Same register-panel geometry as the K-term form, so both can share the tile list.
+        if (fuse_mode != 0 && small && !fin_lds && iters == 2 && (rbucket == 2 || rbucket == 4) && orth_chol &&
+            env_int("PSGD_FIN_PROJ", 1) != 0) {
+            const FinForm f = fin_form(rbucket, false);
+            int smax = 0;
+            for (const MatDesc& d : mats) smax = std::max(smax, fin_geometry(d.n, d.m, f, 0).S);
+            int waves = 0;
+            FinalArgs none{};
+            fin_proj = fin_bucket(smax) > 0 &&
+                       launch_final_odd(dtype, rbucket, kFinProj, fin_bucket(smax), none, 0, nullptr, &waves) ==
+                           hipSuccess &&
+                       waves >= 2;
+        }
         fin_smax = 0;
-        if (fin_ok) {
+        if (fin_ok || fin_proj) {
             const FinForm f = fin_form(rbucket, fin_lds);
             const int64_t elems = fin_lds ? fin_elems_lds : fin_elems;
             // segments per row up to the kernel bucket the widest groups already need
@@ -668,15 +687,18 @@ struct psgd_plan {
         }
         if (!bucket_gend.empty()) build_spans();
     }
-    // the last iteration of `step` runs fused (odd, and every matrix fits)
-    bool fused_final(int64_t step) const { return fin_ok && !even(step, iters - 1); }
+    // the last iteration of `step` runs fused (odd, and every matrix fits); `agg`: the caller
+    // is psgd_aggregate (world size 1, output written), where the projection form also applies
+    bool fused_final(int64_t step, bool agg) const { return (fin_ok || (agg && fin_proj)) && !even(step, iters - 1); }
+    // the fused last iteration takes the projection form
+    bool proj_final(int64_t step, bool agg) const { return agg && fin_proj && !even(step, iters - 1); }
     // an odd iteration before the last one, at world size 1 (fuse): P in the row-resident final
     // kernel in product-only form (no partials, no reduction launch)
     bool fin_prod(int64_t step, int it, bool fuse) const {
         return fuse && fin_ok && fin_grng_ok && it < iters - 1 && !even(step, it) &&
                env_int("PSGD_FIN_PRODUCT", 0) != 0;  // opt-in: neutral-to-slower on cfg5
     }
-    bool fused_final_at(int64_t step, int it) const { return it == iters - 1 && fused_final(step); }
+    bool fused_final_at(int64_t step, int it, bool agg) const { return it == iters - 1 && fused_final(step, agg); }
 
     int upload_tiles() const;
 };
@@ -973,6 +995,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
     p->o_ipc_ptrs = carve(size_t(kMaxRanks) * sizeof(void*));
+    p->o_rq = carve(size_t(std::max<int64_t>(p->fmax, 1)) * sizeof(float));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
@@ -1086,7 +1109,6 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     // opt-in: the in-launch seam measured slower than the k_reduce boundary it replaces on
     // every BASELINE config (profiles/r02/fold_ab.txt; cdna_hip_programming.md §5.6 agrees)
     p->fold = env_int("PSGD_FOLD", 0) != 0;
-    p->orth_chol = env_int("PSGD_ORTH_CHOL", 1) != 0;
     if (p->f64()) {
         if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
         if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
@@ -1220,7 +1242,9 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     const bool fused = fused_norm(p, fuse, it);
     // rank 1, iteration 0, even: the joint norm of the (raw) state P is folded into the even
     // product (per-chunk sums of squares) and its reduction (divide, write normalised P)
-    const bool fused0 = norm0_fold() && p->rbucket == 1 && it == 0 && even && !p->fused_final_at(step, it);
+    const bool fused0 = norm0_fold() && p->rbucket == 1 && it == 0 && even && !p->fused_final_at(step, it, write_out);
+    // projection form of the fused last iteration: its orthonormalisation leaves R' in o_rq
+    const bool proj = it == p->iters - 1 && p->proj_final(step, write_out);
     float* ss = p->dev<float>(p->o_ss);
 
     if (!fused && !fused0) {
@@ -1230,6 +1254,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         oa.state = in;
         oa.hx = p->hist(0, it);
         oa.save = it > 0 ? p->hist(2, it - 1) : nullptr;  // keep the all-reduced factor of it-1
+        oa.rfac = proj ? p->dev<float>(p->o_rq) : nullptr;
         const int nunits = ur[1] - ur[0];
         if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, p->orth_chol, s));
     }
@@ -1249,7 +1274,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     const int32_t* prev_grng = prev_fold    ? p->dev<int32_t>(p->o_grng_strip)
                                : prev_fprod ? p->dev<int32_t>(p->o_grng_fin)
                                             : p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
-    if ((it == p->iters - 1 && p->fused_final(step)) || fprod) {
+    if ((it == p->iters - 1 && p->fused_final(step, write_out)) || fprod) {
         // last iteration, odd: product + residual (+ output at world size 1) in one pass;
         // fprod: an earlier odd iteration, product only
         FinalArgs fa{};
@@ -1273,6 +1298,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
             fa.hx = p->hist(0, it);
         }
         const int nfin = sp.fin[1] - sp.fin[0];
+        if (proj) {  // no error-feedback terms: P_0 and R' only
+            fa.proj_p0 = p->hist(0, 0);
+            fa.proj_r = p->dev<float>(p->o_rq);
+            fill_terms(p, step, 0, fa.res);
+            fa.nres = kFinProj;
+        }
         fa.ntiles = nfin;
         if (fl && write_out && !fprod) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         if (nfin + fa.flat.nitems == 0) return PSGD_OK;
@@ -1282,7 +1313,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (p->fin_lds)
             PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa, nfin, s));
         else
-            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, it, fin_bucket(p->fin_smax), fa, nfin, s));
+            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, fa.nres, fin_bucket(p->fin_smax), fa, nfin, s));
         if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
         return PSGD_OK;
     }
@@ -1404,7 +1435,7 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     }
     aa.nterms = I;
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
-    if (p->fused_final(step)) {
+    if (p->fused_final(step, false)) {
         // the residual was written by the fused last iteration: output only
         aa.ntiles = nt;
         if (nt > 0) PSGD_HIP(launch_lowrank_out(p->dtype, p->rbucket, I, aa, nt, s));
@@ -1686,10 +1717,10 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
     return PSGD_OK;
 }
 
-int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t* fused) {
+int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t aggregate, int32_t* fused) {
     if (!p || !fused) return fail(PSGD_ERR_VALUE, "null argument");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
-    *fused = p->fused_final(step) ? 1 : 0;
+    *fused = p->fused_final(step, aggregate != 0) ? 1 : 0;
     return PSGD_OK;
 }
 
@@ -1727,7 +1758,7 @@ static int aggregate_impl(psgd_plan* p, void* const* grads, void* out, int64_t s
     p->out_now = out;
     for (int it = 0; it < p->iters; ++it)
         if (int st = compress_impl(p, grads, step, it, s, fuse, true, fl, span)) return st;
-    if (p->fused_final(step)) return PSGD_OK;  // output written by the fused last iteration
+    if (p->fused_final(step, true)) return PSGD_OK;  // output written by the fused last iteration
     return decompress_impl(p, grads, out, step, 1, s, fuse, fl, span);
 }
 

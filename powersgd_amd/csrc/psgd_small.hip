@@ -103,8 +103,9 @@ __device__ __forceinline__ void block_sum_nw(A (&v)[NV], A* red) {
     }
 }
 
+// rout (optional): the r x r factor R of the QR (geqr2's upper triangle), row-major
 template <int R, int NT = kBlock>
-__device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau) {
+__device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau, float* rout = nullptr) {
     const int tid = threadIdx.x;
     for (int j = 0; j < r; ++j) {
         float s1[1] = {0.f};
@@ -150,6 +151,13 @@ __device__ void householder_q(float* A, int64_t k, int r, float* red, float* tau
             }
             __syncthreads();
         }
+    }
+    if (rout) {
+        for (int e = tid; e < r * r; e += NT) {
+            const int i = e / r, j = e - (e / r) * r;
+            rout[e] = i <= j ? A[int64_t(i) * r + j] : 0.f;
+        }
+        __syncthreads();  // read before org2r overwrites the upper triangle
     }
     // org2r: Q = H_0 H_1 ... H_{r-1} I[:, :r], built in place, last reflector first
     for (int j = r - 1; j >= 0; --j) {
@@ -269,6 +277,8 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, double* rd
     for (int w = 0; w < NT / 64; ++w) s += rd[w];
     const float nrm = float(sqrt(s));
     const float d = nrm > 1e-16f ? nrm : 1e-16f;  // torch.maximum(norm, eps)
+    if (a.rfac)  // x = (x / d) d: R' = d for every panel of the group
+        for (int c = tid; c < u.count; c += NT) a.rfac[u.off + int64_t(c) * u.k] = d;
     for (int64_t base = tid; base < total; base += int64_t(U) * NT) {
         float x[U];
 #pragma unroll
@@ -1085,13 +1095,20 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
 #pragma unroll
                 for (int c = 0; c < R; ++c) m_sh[i * R + c] = M[i][c] * sgn[c];
             ok_sh = ok ? 1 : 0;
+            if (a.rfac && ok) {  // X = Q (D R): R' = D R
+#pragma unroll
+                for (int i = 0; i < R; ++i)
+#pragma unroll
+                    for (int c = 0; c < R; ++c)
+                        if (i < r && c < r) a.rfac[u.off + i * r + c] = i <= c ? float(sgn[i] * Rm[i][c]) : 0.f;
+            }
         }
     }
     __syncthreads();
     if (!ok_sh) {  // exact Householder (geqr2 + org2r) in place in the history buffer
         for (int64_t i = tid; i < k * r; i += NT) hx[i] = st[i];
         __syncthreads();
-        householder_q<R, NT>(hx, k, r, red, tau);
+        householder_q<R, NT>(hx, k, r, red, tau, a.rfac ? a.rfac + u.off : nullptr);
         for (int64_t i = tid; i < k * r; i += NT) st[i] = hx[i];
         return;
     }

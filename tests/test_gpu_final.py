@@ -10,6 +10,10 @@ registers. These tests pin it three ways:
 * the world-size > 1 code path (psgd_compress writes the residual, psgd_decompress writes
   only the output with k_lowrank_out) driven at world size 1 through the C ABI, against
   the single-call psgd_aggregate.
+Two-iteration rank-2/4 plans take the projection form in psgd_aggregate (output G X X^T,
+residual G - G X X^T, P state G X - P_0 R'^T; exact algebra for I = 2 at world size 1, see
+psgd_final.cuh): checked against the oracle at the same 1e-5, and against the K-term form
+(PSGD_FIN_PROJ=0) through the unfused comparison.
 Shapes cover every row-group form: sub-wave groups (m <= 256), one to four waves, several
 register segments, bf16 rows, rank caps, and a matrix whose rows do not fill a batch.
 """
@@ -38,17 +42,20 @@ def _rel(a, b, scale):
     return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
 
 
-def _make(shapes, rank, iters, dtype=torch.float32, fuse=True):
-    old = os.environ.get("PSGD_FUSE_FINAL")
-    os.environ["PSGD_FUSE_FINAL"] = ("2" if fuse is True else str(int(fuse))) if fuse else "0"  # 2, 3 or 0
+def _make(shapes, rank, iters, dtype=torch.float32, fuse=True, proj=True):
+    env = {"PSGD_FUSE_FINAL": ("2" if fuse is True else str(int(fuse))) if fuse else "0",  # 2, 3 or 0
+           "PSGD_FIN_PROJ": "1" if proj else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dtype) for s in shapes],
                         Config(rank, 0.5, iters, 0))
     finally:
-        if old is None:
-            del os.environ["PSGD_FUSE_FINAL"]
-        else:
-            os.environ["PSGD_FUSE_FINAL"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     return psgd
 
 
@@ -58,14 +65,18 @@ NARROW = [s for s in SHAPES if int(torch.tensor(s[1:]).prod()) <= 2048]
 
 
 # mode: PSGD_FUSE_FINAL for the fused plan (2: register panels allowed at every rank, LDS
-# panels where they do not fit; 3: the LDS-panel kernel k_final_lds forced)
+# panels where they do not fit; 3: the LDS-panel kernel k_final_lds forced); "2k": mode 2
+# with the projection form off (the K-term form at I = 2)
 @pytest.mark.parametrize("rank,iters,narrow,mode", [
     (1, 2, False, 2), (2, 2, False, 2), (1, 1, False, 2), (2, 1, False, 2), (1, 3, False, 2), (1, 4, False, 2),
     (4, 2, False, 2), (2, 3, False, 2), (1, 3, True, 2), (2, 4, True, 2), (2, 2, True, 2),
+    (4, 2, False, "2k"), (2, 2, False, "2k"), (4, 2, True, 2),
     (4, 2, False, 3), (2, 2, False, 3), (4, 1, False, 3), (2, 1, True, 3)])
 def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
     shapes = NARROW if narrow else SHAPES
-    fused = _make(shapes, rank, iters, fuse=mode)
+    proj = mode != "2k"
+    mode = 2 if mode == "2k" else mode
+    fused = _make(shapes, rank, iters, fuse=mode, proj=proj)
     plain = _make(shapes, rank, iters, fuse=False)
     plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
     plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
@@ -98,7 +109,8 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
         plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
     expect_odd_last = sum(((t * iters + iters - 1) % 2) == 1 for t in range(3))
-    if narrow or (rank == 1 and iters <= 2) or mode == 3:  # configurations that must fuse
+    projection = proj and mode == 2 and iters == 2 and rank in (2, 4)
+    if narrow or (rank == 1 and iters <= 2) or mode == 3 or projection:  # configurations that must fuse
         assert n_fused == expect_odd_last, (n_fused, expect_odd_last)
 
 
@@ -125,8 +137,9 @@ def test_split_calls_match_aggregate(rank, iters):
     """psgd_compress (fused last iteration writes the residual) + psgd_decompress
     (k_lowrank_out writes the output): the world-size > 1 sequence, at world size 1."""
     shapes = SHAPES
-    a = _make(shapes, rank, iters)
-    b = _make(shapes, rank, iters)
+    # the split calls have no projection form: compare with psgd_aggregate's K-term form
+    a = _make(shapes, rank, iters, proj=False)
+    b = _make(shapes, rank, iters, proj=False)
     b._powersgd._ps_buffer.copy_(a._powersgd._ps_buffer)
     b._powersgd._qs_buffer.copy_(a._powersgd._qs_buffer)
     ca, cb = a._powersgd, b._powersgd
