@@ -271,11 +271,14 @@ def main():
     mask = psgd.is_compressed_mask
     # which final pass each timed step took (I odd: steps alternate between the fused last odd
     # iteration and k_apply); bytes are averaged over the timed steps
-    nf = sum(codec._plan.fused_final(t, world == 1) for t in range(first_cold, first_cold + a.steps))
+    forms = [codec._plan.fused_final(t, world == 1) for t in range(first_cold, first_cold + a.steps)]
+    nf = sum(1 for f in forms if f)
     frac_f = nf / a.steps
     ab = frac_f * apply_alg_bytes(c, mask, world, True) + (1 - frac_f) * apply_alg_bytes(c, mask, world, False)
     sb = frac_f * step_alg_bytes(c, mask, world, True) + (1 - frac_f) * step_alg_bytes(c, mask, world, False)
-    kf = "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")")
+    kf = ("k_final_proj (fused last odd iteration, projection form: G X, residual G - G X X^T, output G X X^T)"
+          if nf and all(f == 2 for f in forms if f) else
+          "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")"))
     kname = kf if nf == a.steps else "k_apply (fused residual + output)" if nf == 0 else f"{kf} / k_apply, alternating"
 
     def roof(apply_ms, cache):

@@ -238,12 +238,13 @@ class Plan:
     def ipc_sum(self, step: int, stream: int) -> None:
         check(lib().psgd_ipc_sum(self._h, step, stream))
 
-    def fused_final(self, step: int, aggregate: bool = True) -> bool:
-        """True when the last iteration of ``step`` runs fused with the final pass
-        (``aggregate``: in ``psgd_aggregate``, the world-size-1 path; else the building blocks)."""
+    def fused_final(self, step: int, aggregate: bool = True) -> int:
+        """Nonzero when the last iteration of ``step`` runs fused with the final pass: 2 in the
+        projection form, 1 in the K-term form (``aggregate``: in ``psgd_aggregate``, the
+        world-size-1 path; else the building blocks)."""
         f = _i32()
         check(lib().psgd_plan_fused_final(self._h, step, 1 if aggregate else 0, ctypes.byref(f)))
-        return bool(f.value)
+        return int(f.value)
 
     # --- building blocks (paper-code reducer variants, powersgd_amd/reducers.py)
     def product(self, grads, odd: bool, x_ptr: int, y_ptr: int, terms=(), stream: int = 0) -> None:

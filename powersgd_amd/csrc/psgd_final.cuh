@@ -108,6 +108,16 @@ __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c
 // PL (panels in LDS): the factor panels X and Q_0 of the whole matrix live in LDS (`pan`,
 // [m][R] each, R floats per column) instead of per-thread registers, so a rank-4 row needs no
 // register panels and a 1024-thread workgroup keeps 16 waves of rows in flight.
+// Cross-wave row sums (row groups wider than a wave): 0 = dependent LDS reads in wave order,
+// 1 = a component's wave partials loaded together, 2 = wave-minor layout with 16-byte reads.
+// Build-time knob for A/B runs.
+#ifndef PSGD_FIN_XSUM
+#define PSGD_FIN_XSUM 0
+#endif
+
+// P_0 rows of a row block staged in LDS by the projection form: kFinRowsMax (psgd_internal.h)
+constexpr int kProjRows = kFinRowsMax;
+
 // PJ (projection form, two power iterations at world size 1, K = 0): X = orth(Q_0) with
 // Q_0 = X R' (R' = the QR factor the orthonormalisation left in a.proj_r), so the reference's
 // output P_0 Q_0^T + P_1 X^T with P_1 = (G - P_0 Q_0^T) X is exactly G X X^T and the residual
@@ -153,12 +163,18 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         act[s] = s < S && c < m;
         ccol[s] = act[s] ? c : 0;
     }
-    // PJ: R' of this matrix (r x r, row-major at its Q-layout offset; zero outside r x r),
-    // staged in LDS: only the row-group leaders read it, once per row (no registers held)
+    // PJ: R' of this matrix (r x r, row-major at its Q-layout offset; zero outside r x r)
+    // and the block's first kProjRows rows of P_0, staged in LDS: only the row-group leaders
+    // read them, once per row, with no global load (and vmcnt wait) inside the row loop
     if constexpr (PJ) {
         if (tid < R * R) {
             const int c = tid / R, l = tid - (tid / R) * R;
             rqs[tid] = (c < r && l < r) ? a.proj_r[d.qoff + c * r + l] : 0.f;
+        }
+        const int nst = int(row_end - row0) * R;  // the plan keeps row blocks <= kProjRows rows
+        for (int e = tid; e < nst; e += NT) {
+            const int i = e / R, l = e - (e / R) * R;
+            rqs[R * R + e] = l < r ? a.proj_p0[d.poff + (row0 + i) * r + l] : 0.f;
         }
         __syncthreads();
     }
@@ -359,6 +375,46 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
                 for (int c = 0; c < R; ++c) dot[u][c] = sum_within(dot[u][c], Tg);
         } else {
+#if PSGD_FIN_XSUM == 2
+            // partials wave-minor ([u][c][wave]): a component's NW wave partials are NW / 4
+            // consecutive 16-byte LDS reads, all in flight at once, then added in wave order
+            float* buf = red + (b & 1) * NW * RB * R;
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    dot[u][c] = wave_allsum(dot[u][c]);
+                    if (lane == 0) buf[(u * R + c) * NW + wave] = dot[u][c];
+                }
+            __syncthreads();
+            const int w0 = rg * (Tg >> 6), nw = Tg >> 6;
+#pragma unroll
+            for (int u = 0; u < RB; ++u)
+#pragma unroll
+                for (int c = 0; c < R; ++c) {
+                    const float* src = buf + (u * R + c) * NW;
+                    float pw[NW];
+                    if constexpr (NW % 4 == 0) {
+#pragma unroll
+                        for (int w = 0; w < NW; w += 4) {
+                            const v4f q = *reinterpret_cast<const v4f*>(src + w);
+                            pw[w] = q.x;
+                            pw[w + 1] = q.y;
+                            pw[w + 2] = q.z;
+                            pw[w + 3] = q.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) pw[w] = src[w];
+                    }
+                    // row group rg owns waves [w0, w0 + nw): nw is a power of two dividing NW
+                    float sum = 0.f;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w)
+                        if (w >= w0 && w < w0 + nw) sum = (w == w0) ? pw[w] : sum + pw[w];
+                    dot[u][c] = sum;
+                }
+#else
             float* buf = red + (b & 1) * NW * RB * R;
 #pragma unroll
             for (int u = 0; u < RB; ++u)
@@ -373,18 +429,35 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
             for (int u = 0; u < RB; ++u)
 #pragma unroll
                 for (int c = 0; c < R; ++c) {
+#if PSGD_FIN_XSUM == 1
+                    // a component's wave partials read at once (one LDS round trip), added in
+                    // wave order
+                    float pw[NW];
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) pw[w] = buf[(w0 + (w < nw ? w : 0)) * RB * R + u * R + c];
+                    float sum = pw[0];
+#pragma unroll
+                    for (int w = 1; w < NW; ++w)
+                        if (w < nw) sum += pw[w];
+#else
                     float sum = buf[w0 * RB * R + u * R + c];
                     for (int w = 1; w < nw; ++w) sum += buf[(w0 + w) * RB * R + u * R + c];
+#endif
                     dot[u][c] = sum;
                 }
+#endif
         }
         // the local out-factor rows (history + the reference-visible P state, :189-193)
         if (tt == 0) {
 #pragma unroll
             for (int u = 0; u < RB; ++u)
                 if (ib + u < row_end) {
-                    float p0[PJ ? R : 1];  // PJ: this row of P_0 (leaders only, loaded here)
-                    if constexpr (PJ) ld_factor<R>(gconst<float>(a.proj_p0) + d.poff + (ib + u) * r, r, p0);
+                    float p0[PJ ? R : 1];  // PJ: this row of P_0 (LDS; blocks <= kProjRows rows)
+                    if constexpr (PJ) {
+                        const int li = int(ib + u - row0);
+#pragma unroll
+                        for (int l = 0; l < R; ++l) p0[l] = rqs[R * R + li * R + l];
+                    }
 #pragma unroll
                     for (int c = 0; c < R; ++c)
                         if (c < r) {
@@ -398,11 +471,11 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             }
                             a.yloc[e] = y;
                             a.state[e] = y;
-                            ssq = fmaf(y, y, ssq);
+                            if constexpr (!PJ) ssq = fmaf(y, y, ssq);  // PJ: never product-only
                         }
                 }
         }
-        if (a.product_only) return;  // a later iteration forms residual and output
+        if (!PJ && a.product_only) return;  // a later iteration forms residual and output
         // residual (and output at world size 1) from the registers
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -428,7 +501,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                     for (int v = 0; v < 4; ++v) {
                         const float tl = dotr<R>(pr, xs[v]);
                         res[v] = g[u][s][v] - tl;
-                        if (a.write_out) {
+                        if (PJ || a.write_out) {  // PJ: world size 1, always
                             float acc = 0.f;
                             if constexpr (K > 0) {
 #pragma unroll
@@ -441,12 +514,12 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                                     acc = acc + dotr<R>(pa, qb);
                                 }
                             }
-                            o[v] = acc + tl;
+                            o[v] = PJ ? tl : acc + tl;
                         }
                     }
                     const bool ok = valid && act[s];
                     fin_st<T, VEC>(gs, rowe + uint32_t(ccol[s]), ok, ccol[s], m, res);
-                    if (a.write_out) fin_st<T, VEC>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                    if (PJ || a.write_out) fin_st<T, VEC>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
                 }
             }
         }
@@ -464,7 +537,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         load(ga, b + 2);
         if (b + 1 < nb) process(gb, b + 1);
     }
-    if (a.product_only && a.ss_out) {
+    if (!PJ && a.product_only && a.ss_out) {
         // this row block's sum of squares of P: row-group leaders in row-group order (fixed)
         __syncthreads();  // the last batch's row sums may still be read from `red`
         if (tt == 0) red[rg] = ssq;
@@ -483,7 +556,7 @@ __device__ __forceinline__ void final_odd_block(const FinalArgs& a) {
     // batch row sums (2 buffers) and, in product-only mode, one sum of squares per row group
     constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
     __shared__ float red[kRed];
-    __shared__ float rqs[PJ ? R * R : 1];
+    __shared__ float rqs[PJ ? R * R + kProjRows * R : 1];
     // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
     // not in the launch tail); then the row blocks
     const int nf = a.flat.nitems;

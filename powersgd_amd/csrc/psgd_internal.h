@@ -208,6 +208,9 @@ struct FinalArgs {
 };
 // nres value selecting the projection form of the fused final pass (I = 2, world size 1)
 constexpr int kFinProj = 1000;
+// rows per row block of the register-panel final pass (the projection form stages a block's
+// P_0 rows in LDS)
+constexpr int kFinRowsMax = 256;
 
 struct OrthArgs {
     const OrthUnit* units;

@@ -195,6 +195,8 @@ FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int sca
     // a small matrix must still spread over several workgroups
     rows = std::min(rows, std::max(batch, round_up((n + 7) / 8, batch)));
     rows = std::min(rows, round_up(n, batch));
+    if (f.nt == f.tmax)  // register-panel form: at most kFinRowsMax rows (a multiple of batch)
+        rows = std::min(rows, std::max(batch, kFinRowsMax / batch * batch));
     g.rows = int(rows);
     g.ntiles = (n + rows - 1) / rows;
     return g;
@@ -1720,7 +1722,7 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
 int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t aggregate, int32_t* fused) {
     if (!p || !fused) return fail(PSGD_ERR_VALUE, "null argument");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
-    *fused = p->fused_final(step, aggregate != 0) ? 1 : 0;
+    *fused = p->proj_final(step, aggregate != 0) ? 2 : p->fused_final(step, aggregate != 0) ? 1 : 0;
     return PSGD_OK;
 }
 

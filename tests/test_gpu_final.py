@@ -83,7 +83,10 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
     n_fused = 0
     res = [torch.zeros(s) for s in shapes]
     for t in range(3):
-        n_fused += fused._powersgd._plan.fused_final(t)
+        form = fused._powersgd._plan.fused_final(t)
+        n_fused += bool(form)
+        if form:  # 2 = projection form: exactly the two-iteration rank-2/4 register-panel plans
+            assert (form == 2) == (proj and mode == 2 and iters == 2 and rank in (2, 4)), (form, t)
         ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 0.5, iters, 0)
         ora.codec.p_flat.copy_(fused._powersgd._ps_buffer.cpu())
         ora.codec.q_flat.copy_(fused._powersgd._qs_buffer.cpu())

@@ -50,9 +50,9 @@ def main():
         print(f"# {path}")
         for (k, c), v in sorted(acc.items()):
             print(f"{k[:70]:70s} {c:12s} n={len(v):4d} avg={statistics.mean(v):14.1f}")
-            # the final pass: k_final_odd (fused last odd iteration) if the run has it, else k_apply
-            if k.startswith(("psgd::k_final_odd", "psgd::k_apply")) and c in ("FETCH_SIZE", "WRITE_SIZE"):
-                prio = 2 if k.startswith("psgd::k_final_odd") else 1
+            # the final pass: k_final_odd / k_final_proj (fused last odd iteration) if the run has it, else k_apply
+            if k.startswith(("psgd::k_final_odd", "psgd::k_final_proj", "psgd::k_apply")) and c in ("FETCH_SIZE", "WRITE_SIZE"):
+                prio = 2 if k.startswith(("psgd::k_final_odd", "psgd::k_final_proj")) else 1
                 if prio >= traffic.get(c + "_prio", 0):
                     traffic[c] = statistics.mean(v) * 1024 * (2 if c == "FETCH_SIZE" else 1)
                     traffic[c + "_prio"] = prio
