@@ -855,10 +855,11 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     int maxr = 1;
     for (auto& g : p->groups) maxr = std::max(maxr, g.r);
     {
-        // about 1.5k tiles (6 per CU) on large problems, never below 4k elements per tile
+        // about 3k tiles (12 per CU) on large problems, never below 4k elements per tile: the
+        // cold even product on ResNet-50 is fastest at 8k-element tiles (profiles/r02/tile_sweep.txt)
         int64_t total = 0;
         for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
-        const int64_t dflt = std::min<int64_t>(16384, std::max<int64_t>(4096, total / 1536));
+        const int64_t dflt = std::min<int64_t>(16384, std::max<int64_t>(4096, total / 3072));
         p->tile_elems = std::max<int64_t>(1024, env_int("PSGD_TILE_ELEMS", dflt));
     }
     if (maxr > 32) {

@@ -197,6 +197,49 @@ static float time_it(F f, int reps) {
     return ms * 1000.f / reps;  // us per launch
 }
 
+// Even-product access pattern: one workgroup per tile of `rows` rows x 256 columns (64 lanes x
+// 16 B) of an n x m fp32 matrix; wave w reads rows w, w + 4, ... with U rows in flight per lane
+template <int U>
+__global__ __launch_bounds__(256) void k_read_tiles(const float* __restrict__ g, float* out, int n, int m, int rows) {
+    const int nstrip = (m + 255) / 256;
+    const int strip = blockIdx.x % nstrip, chunk = blockIdx.x / nstrip;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = strip * 256 + 4 * lane;
+    const int r0 = chunk * rows, r1 = min(n, r0 + rows);
+    float s = 0.f;
+    if (col < m) {
+        for (int i = r0 + wave; i < r1; i += 4 * U) {
+            v4f x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int rr = i + 4 * u;
+                x[u] = rr < r1 ? *reinterpret_cast<const v4f*>(g + long(rr) * m + col) : v4f{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) s += x[u].x + x[u].y + x[u].z + x[u].w;
+        }
+    }
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
+// Row-major blocks: one workgroup per block of `rows` consecutive full rows, read as one
+// contiguous range (the final pass's / a row-layout product's order)
+template <int U>
+__global__ __launch_bounds__(256) void k_read_rowblk(const v4f* __restrict__ g, float* out, long n4, long per) {
+    const long b0 = long(blockIdx.x) * per, b1 = b0 + per < n4 ? b0 + per : n4;
+    float s = 0.f;
+    for (long b = b0 + threadIdx.x; b < b1; b += 256L * U) {
+        v4f x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long i = b + 256L * u;
+            x[u] = i < b1 ? g[i] : v4f{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) s += x[u].x + x[u].y + x[u].z + x[u].w;
+    }
+    if (s == 12345.f) out[threadIdx.x] = s;
+}
+
 int main() {
     const long bytes = 102228128L / 16 * 16;
     const long n4 = bytes / 16;
@@ -335,6 +378,27 @@ int main() {
                 ++k;
             }, 40);
             printf("COLD read+r1w2  grid %5d  %7.2f us  %6.0f GB/s\n", gr, t, 4 * bytes / t / 1e3);
+        }
+        // even-product tile pattern vs contiguous row blocks, cold, 5120 x 4608 and 49152 x 512
+        {
+            struct Sh { int n, m; };
+            for (Sh sh : {Sh{5120, 4608}, Sh{49152, 512}, Sh{20480, 1152}}) {
+                for (int rows : {32, 64, 128}) {
+                    const int nstrip = (sh.m + 255) / 256, nchunk = (sh.n + rows - 1) / rows;
+                    const float* gf = (const float*)gs[k % NS];
+                    float t = time_it([&] { k_read_tiles<4><<<nstrip * nchunk, 256>>>((const float*)gs[k % NS], sink, sh.n, sh.m, rows); ++k; }, 40);
+                    (void)gf;
+                    const double nb = double(sh.n) * sh.m * 4;
+                    printf("COLD tiles n %5d m %4d rows %3d grid %6d  %7.2f us  %6.0f GB/s\n", sh.n, sh.m, rows,
+                           nstrip * nchunk, t, nb / t / 1e3);
+                    const long per = long(rows) * sh.m / 4;
+                    const long n4s = long(sh.n) * sh.m / 4;
+                    const int gr = int((n4s + per - 1) / per);
+                    t = time_it([&] { k_read_rowblk<4><<<gr, 256>>>(gs[k % NS], sink, n4s, per); ++k; }, 40);
+                    printf("COLD rowblk n %5d m %4d rows %3d grid %6d  %7.2f us  %6.0f GB/s\n", sh.n, sh.m, rows, gr, t,
+                           nb / t / 1e3);
+                }
+            }
         }
         for (int i = 0; i < NS; ++i) {
             CK(hipFree(gs[i]));
