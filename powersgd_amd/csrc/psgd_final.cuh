@@ -144,6 +144,46 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                                                         0x00020000);
     const gptr<const float> X = gconst<float>(a.x) + d.qoff;
 
+    int32_t ccol[SMAX];
+    bool act[SMAX];
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+        const int32_t c = (s * Tg + tt) * 4;
+        act[s] = s < S && c < m;
+        ccol[s] = act[s] ? c : 0;
+    }
+    // one batch: rows ib .. ib + RB of row group rg, with their error-feedback factor rows.
+    // Every load of a batch is issued unconditionally (rows past the block end and
+    // segments past the row end load 0 through kOob / clamped factor rows), so the number
+    // of loads in flight is the same on every path and the waits stay counted, not full
+    struct Batch {
+        float g[RB][SMAX][4];
+        float ap[KC][RB][R];
+    };
+    auto load = [&](Batch& bt, int b) {
+        const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s)
+                fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, bt.g[u][s]);
+        }
+        if constexpr (K > 0) {
+#pragma unroll
+            for (int u = 0; u < RB; ++u) {
+                const int64_t ic = ib + u < row_end ? ib + u : row0;  // factor rows: clamped
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic * r, r, bt.ap[k][u]);
+            }
+        }
+    };
+    // The first batch's gradient rows go out before the factor panels, the norm and the
+    // projection rows are loaded: a small block's prologue (panels, norm partials, P_0 rows:
+    // dependent round trips) then overlaps the gradient's HBM latency instead of preceding it.
+    Batch ga, gb;
+    load(ga, 0);
     // rank-1 joint norm of the raw in-factor (world size 1, fused): x / max(||x||, eps)
     const bool norm = a.ss_in != nullptr;
     const float dn = norm ? group_norm_ss(a.ss_in, a.grng_in, d.group) : 1.f;
@@ -155,14 +195,6 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         }
     }
 
-    int32_t ccol[SMAX];
-    bool act[SMAX];
-#pragma unroll
-    for (int s = 0; s < SMAX; ++s) {
-        const int32_t c = (s * Tg + tt) * 4;
-        act[s] = s < S && c < m;
-        ccol[s] = act[s] ? c : 0;
-    }
     // PJ: R' of this matrix (r x r, row-major at its Q-layout offset; zero outside r x r)
     // and the block's first kProjRows rows of P_0, staged in LDS: only the row-group leaders
     // read them, once per row, with no global load (and vmcnt wait) inside the row loop
@@ -286,33 +318,6 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         }
     };
 
-    // one batch: rows ib .. ib + RB of row group rg, with their error-feedback factor rows.
-    // Every load of a batch is issued unconditionally (rows past the block end and
-    // segments past the row end load 0 through kOob / clamped factor rows), so the number
-    // of loads in flight is the same on every path and the waits stay counted, not full
-    struct Batch {
-        float g[RB][SMAX][4];
-        float ap[KC][RB][R];
-    };
-    auto load = [&](Batch& bt, int b) {
-        const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
-#pragma unroll
-            for (int s = 0; s < SMAX; ++s)
-                fin_ld<T, VEC>(gs, rowe + uint32_t(ccol[s]), act[s] && ib + u < row_end, ccol[s], m, bt.g[u][s]);
-        }
-        if constexpr (K > 0) {
-#pragma unroll
-            for (int u = 0; u < RB; ++u) {
-                const int64_t ic = ib + u < row_end ? ib + u : row0;  // factor rows: clamped
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + ic * r, r, bt.ap[k][u]);
-            }
-        }
-    };
     // segments past S load zeros (kOob) and drop their stores; their arithmetic is skipped
     // by a uniform branch
     auto seg_on = [&](int s) { return s < S; };
@@ -529,8 +534,6 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     // synchronises and stores (the workgroup barrier no longer idles the memory system)
     const int64_t rows = row_end - row0;
     const int nb = int((rows + int64_t(RGS) * RB - 1) / (int64_t(RGS) * RB));
-    Batch ga, gb;
-    load(ga, 0);
     for (int b = 0; b < nb; b += 2) {
         load(gb, b + 1);
         process(ga, b);

@@ -58,10 +58,14 @@ struct Tile {
 };
 
 // Reduction item for the partial-sum pass: 256 consecutive factor elements of one matrix.
-constexpr int kRedElems = 64;  // factor elements per reduction item (one per lane)
+constexpr int kRedElems = 64;  // fp64 plans: factor elements per reduction item (one per lane)
+constexpr int kRedItem = 256;  // fp32/bf16 plans: at most this many factor elements per reduction item
+constexpr int kRedWide = 64;   // ... when an element has at most this many partials (else 64)
 
 struct RedItem {
     int32_t mat, start;
+    int32_t per;  // fp32/bf16 plans: elements per lane (4: 256-element item; 1: 64 elements,
+                  // for factors with many partials, where 4 per lane is one CU's bandwidth)
 };
 
 // Orthonormalisation unit: rank 1 -> one shape GROUP (joint norm over count*k values);

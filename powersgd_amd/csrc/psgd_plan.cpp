@@ -936,9 +936,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
         const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
         const OddGeom og = odd_geometry(md.n, md.m, p->tile_elems);
-        md.part_even = p->part_floats;
+        // 16-byte aligned partial slabs (k_reduce's vector loads)
+        md.part_even = p->part_floats = (p->part_floats + 3) & ~int64_t(3);
         p->part_floats += std::max(a.part_even, b.part_even);
-        md.part_odd = p->part_floats;
+        md.part_odd = p->part_floats = (p->part_floats + 3) & ~int64_t(3);
         p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
         p->tiles_cap += std::max(a.ntiles, b.ntiles);
         p->slots_cap += std::max(a.nstrip, b.nstrip);
@@ -953,8 +954,13 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
             p->grng_odd.push_back(int32_t(p->red_odd.size()));
             p->grng_odd.push_back(0);
         }
-        for (int64_t s = 0; s < md.m * md.r; s += kRedElems) p->red_even.push_back(RedItem{int32_t(i), int32_t(s)});
-        for (int64_t s = 0; s < md.n * md.r; s += kRedElems) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s)});
+        // fp32/bf16: 4 elements per lane unless an element has more than kRedWide partials
+        // (any geometry set_vec may pick), whose 4-wide item would be one CU's bandwidth
+        const int np_even = std::max(a.nchunk, b.nchunk);
+        const int np_odd = std::max({a.nstrip, b.nstrip, og.nstrip});
+        const int pe = p->f64() || np_even > kRedWide ? 1 : 4, po = p->f64() || np_odd > kRedWide ? 1 : 4;
+        for (int64_t s = 0; s < md.m * md.r; s += 64 * pe) p->red_even.push_back(RedItem{int32_t(i), int32_t(s), pe});
+        for (int64_t s = 0; s < md.n * md.r; s += 64 * po) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s), po});
         p->grng_even.back() = int32_t(p->red_even.size());
         p->grng_odd.back() = int32_t(p->red_odd.size());
     }

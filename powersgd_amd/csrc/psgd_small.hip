@@ -1549,36 +1549,53 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, bool 
 // Sums the partials of each factor element in a FIXED order (row chunks for even
 // iterations, column strips for odd ones): bitwise reproducible, no atomics.
 
-// One item = kRedElems (64) consecutive elements of one factor; wave w adds the partials
+// One item = 64 * per consecutive elements of one factor (per = 4, or 1 for factors with
+// many partials: RedItem::per). per = 4: one 16-byte load per partial when the factor length
+// and its partial slab are 16-byte aligned (lane l owns elements 4l .. 4l+3), else four
+// 256-byte wave loads (lane l owns l, l+64, l+128, l+192). Wave w adds the partials
 // [w*np/4, (w+1)*np/4) of each element in order, then wave 0 adds the four wave sums in
-// order: every element is summed in the same fixed order on every run.
+// order: every element is summed in the same fixed order on every run, whatever the layout.
+// (Four times fewer workgroups than one element per lane: the whole ResNet-50 reduction is
+// resident at once instead of taking two rounds of descriptor + partial round trips.)
+__device__ __forceinline__ int64_t red_elem(bool vec, int64_t start, int lane, int j) {
+    return vec ? start + 4 * lane + j : start + lane + 64 * j;
+}
+
 __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
-    __shared__ float red[kWaves * kRedElems];
+    __shared__ float red[kWaves * kRedItem];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (int(blockIdx.x) >= a.nmain) {  // fused normalisation of the in-factor (rank 1)
         if (wave != 0) return;
         const RedItem it = a.nitems[blockIdx.x - a.nmain];
         const MatDesc d = a.mats[it.mat];
         const int64_t len = (a.even ? d.n : d.m) * d.r;
-        const int64_t e = int64_t(it.start) + lane;
-        const int64_t i = (a.even ? d.poff : d.qoff) + (e < len ? e : 0);
-        float x = a.raw[i];  // in flight together with the norm's loads
+        const int64_t base = a.even ? d.poff : d.qoff;
+        float x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // in flight together with the norm's loads
+            const int64_t e = red_elem(false, it.start, lane, j);
+            x[j] = a.raw[base + (e < len ? e : 0)];
+        }
         const float dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
-        if (e < len) {
-            x = x / dn;  // matrix.div_(max(norm, eps))
-            a.xstate[i] = x;
-            a.hx[i] = x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t e = red_elem(false, it.start, lane, j);
+            if (j < it.per && e < len) {
+                const float v = x[j] / dn;  // matrix.div_(max(norm, eps))
+                a.xstate[base + e] = v;
+                a.hx[base + e] = v;
+            }
         }
         return;
     }
     const RedItem it = a.items[blockIdx.x];
     const MatDesc d = a.mats[it.mat];
     const int64_t len = (a.even ? d.m : d.n) * d.r;
-    const int64_t e = int64_t(it.start) + lane;
-    const int64_t ec = e < len ? e : 0;
+    const int64_t poff = a.even ? d.part_even : d.part_odd;
+    const int per = it.per;
+    const bool vec = per == 4 && ((len | poff) & 3) == 0;  // uniform per workgroup
     const int np = a.even ? d.nchunk : d.odd_nstrip;
     const int c0 = wave * np / kWaves, c1 = (wave + 1) * np / kWaves;
-    const float* p = a.part + (a.even ? d.part_even : d.part_odd) + ec;
     // wave 0's first group-norm loads go out before the partials' (group_norm_ss's order:
     // lane-strided sums from 0, then the wave tree), so the two round trips overlap
     const bool nrm = a.ss_in != nullptr && wave == 0;
@@ -1589,37 +1606,94 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         ge = a.grng_in[2 * d.group + 1];
         ssv = gb + lane < ge ? a.ss_in[gb + lane] : 0.f;
     }
-    float s = 0.f;
-    // loads issued kRedBatch at a time (clamped, unconditional): the partials were just written
-    // on other XCDs, so each batch is one MALL round trip; small plans have up to 256 partials
-    // per element (64 per wave), which 8-deep batches turned into 8 serial round trips
-    constexpr int kRedBatch = 16;
-    for (int c = c0; c < c1; c += kRedBatch) {
-        float v[kRedBatch];
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    // loads issued 16 at a time (clamped, unconditional): the partials were just written on
+    // other XCDs, so each batch is one MALL round trip
+    const gptr<const float> pb = gconst<float>(a.part) + poff;
+    if (vec) {
+        const int64_t e0 = red_elem(true, it.start, lane, 0);
+        const gptr<const float> p = pb + (e0 < len ? e0 : 0);
+        constexpr int kB = 16;
+        for (int c = c0; c < c1; c += kB) {
+            float v[kB][4];
 #pragma unroll
-        for (int q = 0; q < kRedBatch; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
+            for (int q = 0; q < kB; ++q) {
+                const v4f x = *(gptr<const v4f>)(p + int64_t(c + q < c1 ? c + q : c0) * len);
+                v[q][0] = x.x; v[q][1] = x.y; v[q][2] = x.z; v[q][3] = x.w;
+            }
 #pragma unroll
-        for (int q = 0; q < kRedBatch; ++q) {
-            keep(v[q]);
-            s += c + q < c1 ? v[q] : 0.f;
+            for (int q = 0; q < kB; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    keep(v[q][j]);
+                    s[j] += c + q < c1 ? v[q][j] : 0.f;
+                }
+        }
+    } else if (per == 4) {
+        int64_t ec[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t e = red_elem(false, it.start, lane, j);
+            ec[j] = e < len ? e : 0;
+        }
+        constexpr int kB = 4;
+        for (int c = c0; c < c1; c += kB) {
+            float v[kB][4];
+#pragma unroll
+            for (int q = 0; q < kB; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[q][j] = pb[int64_t(c + q < c1 ? c + q : c0) * len + ec[j]];
+#pragma unroll
+            for (int q = 0; q < kB; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    keep(v[q][j]);
+                    s[j] += c + q < c1 ? v[q][j] : 0.f;
+                }
+        }
+    } else {
+        const int64_t e = int64_t(it.start) + lane;
+        const gptr<const float> p = pb + (e < len ? e : 0);
+        constexpr int kB = 16;
+        for (int c = c0; c < c1; c += kB) {
+            float v[kB];
+#pragma unroll
+            for (int q = 0; q < kB; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
+#pragma unroll
+            for (int q = 0; q < kB; ++q) {
+                keep(v[q]);
+                s[0] += c + q < c1 ? v[q] : 0.f;
+            }
         }
     }
-    red[wave * kRedElems + lane] = s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < per) red[wave * kRedItem + j * 64 + lane] = s[j];
     __syncthreads();
     if (wave != 0) return;
-    s = ((red[lane] + red[kRedElems + lane]) + red[2 * kRedElems + lane]) + red[3 * kRedElems + lane];
+    float nv = 1.f;
     if (nrm) {
         for (int i = gb + lane + 64; i < ge; i += 64) ssv += a.ss_in[i];
-        const float nv = sqrtf(wave_allsum(ssv));
-        s = s / (nv > 1e-16f ? nv : 1e-16f);  // G^T (x / d) == (G^T x) / d up to rounding
+        nv = sqrtf(wave_allsum(ssv));
+        nv = nv > 1e-16f ? nv : 1e-16f;
     }
-    if (e < len) {
-        const int64_t dst = (a.even ? d.qoff : d.poff) + e;
-        a.yloc[dst] = s;
-        a.state[dst] = s;
+    const int64_t dbase = a.even ? d.qoff : d.poff;
+    float sq = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j >= per) break;
+        const int o = j * 64 + lane;
+        float t = ((red[o] + red[kRedItem + o]) + red[2 * kRedItem + o]) + red[3 * kRedItem + o];
+        if (nrm) t = t / nv;  // G^T (x / d) == (G^T x) / d up to rounding
+        const int64_t e = red_elem(vec, it.start, lane, j);
+        if (e < len) {
+            a.yloc[dbase + e] = t;
+            a.state[dbase + e] = t;
+            sq = fmaf(t, t, sq);
+        }
     }
     if (a.ss_out) {  // this output is the next iteration's in-factor: its sum of squares
-        const float v = wave_allsum(e < len ? s * s : 0.f);
+        const float v = wave_allsum(sq);
         if (lane == 0) a.ss_out[blockIdx.x] = v;
     }
 }
