@@ -185,7 +185,8 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     Batch ga, gb;
     load(ga, 0);
     // rank-1 joint norm of the raw in-factor (world size 1, fused): x / max(||x||, eps)
-    const bool norm = a.ss_in != nullptr;
+    // (rank-1 plans only: fused_norm, psgd_plan.cpp; compile-time false above rank 1)
+    const bool norm = R == 1 && a.ss_in != nullptr;
     const float dn = norm ? group_norm_ss(a.ss_in, a.grng_in, d.group) : 1.f;
     if (norm && t.chunk == 0) {  // row block 0 publishes this matrix's normalised in-factor
         for (int64_t e = tid; e < d.m * r; e += NT) {
@@ -279,6 +280,9 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                 for (int c = 0; c < R; ++c) {
                     const float w = norm ? xq[s][v][c] / dn : xq[s][v][c];  // matrix.div_ (:6)
                     xq[s][v][c] = (act[s] && ccol[s] + v < m) ? w : 0.f;
+                    // rank 1, pinned: LLVM otherwise sinks the division and the select into
+                    // the row loop and re-executes them on every batch
+                    if constexpr (R == 1) keep(xq[s][v][c]);
                 }
     }
     // factor values of the 4 columns of segment s: registers, or R LDS vector reads

@@ -991,7 +991,9 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
                 for (int b = c; b < R; ++b) g[e++] += double(x[q][c]) * double(x[q][b]);
         }
     }
+    PSGD_STAMP(11);
     block_sum_f64<NG, NT / 64>(g, redd);
+    PSGD_STAMP(12);
 
     // The r x r work (Cholesky, R^-1, LAPACK signs) is a serial fp64 latency chain: wave 0
     // alone runs it (the other waves would only compete for the fp64 pipes) and publishes
@@ -1105,6 +1107,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
         }
     }
     __syncthreads();
+    PSGD_STAMP(13);
     if (!ok_sh) {  // exact Householder (geqr2 + org2r) in place in the history buffer
         for (int64_t i = tid; i < k * r; i += NT) hx[i] = st[i];
         __syncthreads();
@@ -1152,13 +1155,16 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
     __shared__ double redd[NT / 64 * (R * (R + 1) / 2)];
     __shared__ float red[NT / 64 * R];
     __shared__ float tau[(R + 3) / 4 * 4];
+    PSGD_STAMP(9);
     const OrthUnit u = a.units[blockIdx.x];
+    PSGD_STAMP(10);
     if (u.r == 1)  // rank-1 group of a mixed-rank plan: the reference's joint norm, not QR
         orth_joint_norm<NT>(a, u, redd);
     else if (u.r == R)
         orth_chol_panel<R, R>(a, u, redd, red, tau);
     else
         orth_chol_panel<R, 0>(a, u, redd, red, tau);
+    PSGD_STAMP(14);
 }
 
 // ------------------------------------------- Cholesky-QR for ranks 9-16 on fp64 MFMA ----
