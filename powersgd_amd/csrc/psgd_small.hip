@@ -949,9 +949,13 @@ struct CholNT {
 // RC = R: the panel has exactly R columns (compile-time rank: the r x r arithmetic is
 // branch-free straight-line fp64 that the compiler interleaves; it is a serial latency
 // chain per workgroup, so this matters); RC = 0: any r <= R at run time.
+// Gram sums through LDS (NT x NG fp64 partials: 40 KB at rank 4) for r <= 4
+template <int R>
+constexpr bool kGramLds = R <= 4;
+
 template <int R, int RC>
 __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUnit& u, double* redd, float* red,
-                                                float* tau) {
+                                                float* tau, double* gpart, float* top_sh) {
     constexpr int NG = R * (R + 1) / 2;
     constexpr int NT = CholNT<R>::value;
     const int r = RC > 0 ? RC : u.r;
@@ -984,6 +988,10 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
                 x[q][c] = i < k ? x[q][c] : 0.f;
             }
             if (sv && i < k) st_row<R>(sv + i * r, r, x[q]);
+            if (kGramLds<R> && i < r) {  // the top r rows: the sign recursion's input, from LDS
+#pragma unroll
+                for (int c = 0; c < R; ++c) top_sh[i * R + c] = x[q][c];
+            }
             int e = 0;
 #pragma unroll
             for (int c = 0; c < R; ++c)
@@ -992,7 +1000,35 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
         }
     }
     PSGD_STAMP(11);
-    block_sum_f64<NG, NT / 64>(g, redd);
+    if constexpr (kGramLds<R>) {
+        // workgroup Gram sums: every thread's NG partials to LDS (entry-major), then wave w
+        // sums entries w, w + NW, ... (lane l: threads l, l + 64, ... in order, then the wave
+        // tree): at most two fp64 wave reductions per wave instead of NG (the DPP trees of NG
+        // fp64 values on every wave were ~40 % of a small panel's kernel time). Fixed order.
+        constexpr int NW = NT / 64;
+#pragma unroll
+        for (int e = 0; e < NG; ++e) gpart[e * NT + tid] = g[e];
+        __syncthreads();
+        const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+        for (int e0 = 0; e0 < NG; e0 += NW) {
+            const int e = e0 + wave;
+            if (e < NG) {
+                double t = gpart[e * NT + lane];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) t += gpart[e * NT + w * 64 + lane];
+                t = wave_allsum_f64(t);
+                if (lane == 0) redd[e] = t;
+            }
+        }
+        __syncthreads();
+        if ((tid >> 6) == 0) {
+#pragma unroll
+            for (int e = 0; e < NG; ++e) g[e] = redd[e];
+        }
+    } else {
+        block_sum_f64<NG, NT / 64>(g, redd);
+    }
     PSGD_STAMP(12);
 
     // The r x r work (Cholesky, R^-1, LAPACK signs) is a serial fp64 latency chain: wave 0
@@ -1002,6 +1038,8 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     __shared__ int ok_sh;
     if ((tid >> 6) == 0) {
         double Rm[R][R];
+        double inv[R];  // 1 / R_jj: one division per column, products elsewhere (the chain is
+                        // serial; each fp64 division is a ~10-instruction dependent sequence)
         bool ok = true;
         {
             double G[R][R];
@@ -1021,6 +1059,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
             }
 #pragma unroll
             for (int j = 0; j < R; ++j) {
+                inv[j] = 1.0;
                 if (j < r) {
                     double piv = G[j][j];
 #pragma unroll
@@ -1029,6 +1068,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
                     ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
                     const double d = sqrt(piv > 0.0 ? piv : 1.0);
                     Rm[j][j] = d;
+                    inv[j] = 1.0 / d;
 #pragma unroll
                     for (int b = 0; b < R; ++b)
                         if (b > j && b < r) {
@@ -1036,7 +1076,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
 #pragma unroll
                             for (int l = 0; l < R; ++l)
                                 if (l < j) v -= Rm[l][j] * Rm[l][b];
-                            Rm[j][b] = v / d;
+                            Rm[j][b] = v * inv[j];
                         }
                 }
             }
@@ -1051,7 +1091,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
 #pragma unroll
                 for (int l = 0; l < R; ++l)
                     if (l > i && l < r) v -= Rm[i][l] * M[l][c];
-                M[i][c] = (i < r && c < r) ? v / Rm[i][i] : 0.0;
+                M[i][c] = (i < r && c < r) ? v * inv[i] : 0.0;
             }
         }
         // LAPACK column signs from the top block T = X[0:r] M
@@ -1059,7 +1099,12 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             float x[R];
-            ld_row<R>(st + int64_t(i < r ? i : 0) * r, r, x);
+            if constexpr (kGramLds<R>) {
+#pragma unroll
+                for (int c = 0; c < R; ++c) x[c] = top_sh[(i < r ? i : 0) * R + c];  // written before the barrier
+            } else {
+                ld_row<R>(st + int64_t(i < r ? i : 0) * r, r, x);
+            }
 #pragma unroll
             for (int c = 0; c < R; ++c) {
                 double v = 0.0;
@@ -1079,10 +1124,11 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
                 ok = ok && !(j < k - 1 && fabs(T[j][j]) > 1.0 - kSignTol);
                 sgn[j] = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
                 T[j][j] -= sgn[j];
+                const double ip = 1.0 / T[j][j];
 #pragma unroll
                 for (int i = 0; i < R; ++i)
                     if (i > j && i < r) {
-                        const double l = T[i][j] / T[j][j];
+                        const double l = T[i][j] * ip;
 #pragma unroll
                         for (int b = 0; b < R; ++b)
                             if (b > j && b < r) T[i][b] -= l * T[j][b];
@@ -1156,14 +1202,16 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
     __shared__ float red[NT / 64 * R];
     __shared__ float tau[(R + 3) / 4 * 4];
     PSGD_STAMP(9);
+    __shared__ double gpart[kGramLds<R> ? NT * (R * (R + 1) / 2) : 1];
+    __shared__ float top_sh[R * R];
     const OrthUnit u = a.units[blockIdx.x];
     PSGD_STAMP(10);
     if (u.r == 1)  // rank-1 group of a mixed-rank plan: the reference's joint norm, not QR
         orth_joint_norm<NT>(a, u, redd);
     else if (u.r == R)
-        orth_chol_panel<R, R>(a, u, redd, red, tau);
+        orth_chol_panel<R, R>(a, u, redd, red, tau, gpart, top_sh);
     else
-        orth_chol_panel<R, 0>(a, u, redd, red, tau);
+        orth_chol_panel<R, 0>(a, u, redd, red, tau, gpart, top_sh);
     PSGD_STAMP(14);
 }
 
