@@ -178,6 +178,26 @@ struct ReduceArgs {
     float* xstate;
     float* hx;
     float* ss_out;       // per-item sum of squares of this reduction's output (or null)
+    // Folded orthonormalisation (projection form, k_orth_chain): per item the upper Gram of
+    // its output rows (kGramStride fp64 entries, rank gram_r in {2, 4}), or null
+    double* gram;
+    int32_t gram_r;
+};
+
+constexpr int kGramStride = 10;  // fp64 Gram entries per reduction item (rank <= 4)
+
+// k_orth_chain: Cholesky-QR of each Q panel from the reduction's Gram partials (no Gram pass
+// over the panel), the panel rows split over several workgroups that each run the r x r chain
+// and apply X = raw M to their slice. Fallback panels (ill-conditioned, unreflected columns):
+// the slice-0 workgroup runs the exact Householder recursion on the whole panel.
+struct ChainArgs {
+    const OrthUnit* units;
+    const int32_t* uitems;  // per unit: [begin, end) of its reduction items
+    const double* gram;     // kGramStride per item
+    const float* raw;       // Q layout: the reduced (raw) factor
+    float* state;           // Q state: X
+    float* hx;              // X history
+    float* rfac;            // Q layout: R' (r x r) at each unit's offset
 };
 
 // Fused LAST iteration when it is odd (P = G_k X): a row group holds whole rows in
@@ -209,6 +229,7 @@ struct FinalArgs {
     // projection form (nres = kFinProj, see psgd_final.cuh): P_0 rows and R' per matrix
     const float* proj_p0;  // P layout
     const float* proj_r;   // Q layout: R' (r x r, row-major) at each matrix's qoff
+
 };
 // nres value selecting the projection form of the fused final pass (I = 2, world size 1)
 constexpr int kFinProj = 1000;
@@ -283,6 +304,7 @@ hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArg
 hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s);
 hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t max_rows, bool chol, hipStream_t s);
+hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, int R, hipStream_t s);
 // paper-code Gram-Schmidt (gradient_reducers.py:945-956) on one panel per unit, per matrix
 hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);

@@ -449,6 +449,13 @@ struct psgd_plan {
     int ipc_world = 0, ipc_rank = -1;
     size_t o_ipc_ptrs = 0;
     size_t o_rq = 0;  // R' of the last iteration's in-factor panels (projection form), Q layout
+    // folded orthonormalisation of the projection form's Q panels (k_orth_chain): every Q unit
+    // a single panel of exactly rbucket in {2, 4} columns; per-item Gram partials and per-unit
+    // item ranges
+    bool qfold_ok = false;
+    size_t o_gram = 0, o_uitems = 0;
+    std::vector<int32_t> uitems, red_even_b, red_even_e;
+    bool qfold(int64_t step, bool agg) const { return qfold_ok && iters == 2 && proj_final(step, agg); }
     // World-size-1 steps as HIP graphs (psgd_plan_set_graphs): one captured graph per distinct
     // (pointer-table slots, output pointers, parity class), replayed with one launch; the buckets
     // (when set and overlap is on) run on two side streams forked inside the graph.
@@ -959,7 +966,9 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         const int np_even = std::max(a.nchunk, b.nchunk);
         const int np_odd = std::max({a.nstrip, b.nstrip, og.nstrip});
         const int pe = p->f64() || np_even > kRedWide ? 1 : 4, po = p->f64() || np_odd > kRedWide ? 1 : 4;
+        p->red_even_b.push_back(int32_t(p->red_even.size()));
         for (int64_t s = 0; s < md.m * md.r; s += 64 * pe) p->red_even.push_back(RedItem{int32_t(i), int32_t(s), pe});
+        p->red_even_e.push_back(int32_t(p->red_even.size()));
         for (int64_t s = 0; s < md.n * md.r; s += 64 * po) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s), po});
         p->grng_even.back() = int32_t(p->red_even.size());
         p->grng_odd.back() = int32_t(p->red_odd.size());
@@ -980,6 +989,23 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->set_f64_tiles();  // fp64: its own kernels and tiles (psgd_f64.hip), no fused forms
     else
         p->set_vec(p->base_vec);
+    // folded orthonormalisation (projection form): every Q unit one panel of rbucket columns
+    p->qfold_ok = !p->f64() && (p->rbucket == 2 || p->rbucket == 4) && !p->units_q.empty() &&
+                  env_int("PSGD_QFOLD", 1) != 0;
+    for (const OrthUnit& u : p->units_q) p->qfold_ok = p->qfold_ok && u.r == p->rbucket && u.count == 1;
+    if (p->qfold_ok) {
+        for (const OrthUnit& u : p->units_q) {
+            int32_t b = -1, e = -1;
+            for (size_t i = 0; i < p->mats.size(); ++i)
+                if (p->mats[i].qoff == u.off) {
+                    b = p->red_even_b[i];
+                    e = p->red_even_e[i];
+                }
+            p->qfold_ok = p->qfold_ok && b >= 0;
+            p->uitems.push_back(b);
+            p->uitems.push_back(e);
+        }
+    }
 
     size_t off = 0;
     auto carve = [&](size_t bytes) {
@@ -1028,6 +1054,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_f64_partoff = carve(std::max<size_t>(p->f64_part_off.size(), 1) * sizeof(int64_t));
     p->o_f64_part = carve(size_t(std::max<int64_t>(p->f64_part, 1)) * sizeof(double));
     p->o_part = carve(size_t(p->part_floats) * sizeof(float));
+    if (p->qfold_ok) {
+        p->o_gram = carve(p->red_even.size() * kGramStride * sizeof(double));
+        p->o_uitems = carve(p->uitems.size() * sizeof(int32_t));
+    }
     p->ws_bytes = off;
     *out_plan = p;
     return PSGD_OK;
@@ -1107,6 +1137,8 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     if (int st = upload(p->dev<void>(p->o_munits_p), p->munits_p.data(), p->munits_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_munits_q), p->munits_q.data(), p->munits_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
+    if (p->qfold_ok)
+        if (int st = upload(p->dev<void>(p->o_uitems), p->uitems.data(), p->uitems.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
     if (int st = upload(p->dev<void>(p->o_ss0_base), p->ss0_base.data(), p->ss0_base.size() * sizeof(int32_t))) return st;
@@ -1254,9 +1286,23 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     const bool fused0 = norm0_fold() && p->rbucket == 1 && it == 0 && even && !p->fused_final_at(step, it, write_out);
     // projection form of the fused last iteration: its orthonormalisation leaves R' in o_rq
     const bool proj = it == p->iters - 1 && p->proj_final(step, write_out);
+    // folded orthonormalisation of the projection form: the even reduction leaves Gram
+    // partials and k_orth_chain (no Gram pass, panel rows over several workgroups) replaces
+    // k_orth_chol
+    const bool qf = p->qfold(step, write_out);
     float* ss = p->dev<float>(p->o_ss);
 
-    if (!fused && !fused0) {
+    if (qf && proj) {
+        ChainArgs ca{};
+        ca.units = p->dev<OrthUnit>(p->o_units_q) + sp.uq[0];
+        ca.uitems = p->dev<int32_t>(p->o_uitems) + 2 * sp.uq[0];
+        ca.gram = p->dev<double>(p->o_gram);
+        ca.raw = p->hist(1, it - 1);  // the even iteration's reduced Q (k_reduce's yloc)
+        ca.state = in;
+        ca.hx = p->hist(0, it);
+        ca.rfac = p->dev<float>(p->o_rq);
+        PSGD_HIP(launch_orth_chain(ca, sp.uq[1] - sp.uq[0], p->panel_q, p->rbucket, s));
+    } else if (!fused && !fused0) {
         OrthArgs oa{};
         const int32_t* ur = even ? sp.up : sp.uq;
         oa.units = p->dev<OrthUnit>(even ? p->o_units_p : p->o_units_q) + ur[0];
@@ -1310,6 +1356,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (proj) {  // no error-feedback terms: P_0 and R' only
             fa.proj_p0 = p->hist(0, 0);
             fa.proj_r = p->dev<float>(p->o_rq);
+
             fill_terms(p, step, 0, fa.res);
             fa.nres = kFinProj;
         }
@@ -1407,6 +1454,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     }
     // ss_out is indexed by the launch's block (item) index: offset like the item list
     if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters) ra.ss_out = ss + size_t(it & 1) * p->ss_stride + rr[0];
+    if (qf && even && it + 2 == p->iters) {  // the Q panels' Gram for k_orth_chain
+        ra.gram = p->dev<double>(p->o_gram) + size_t(rr[0]) * kGramStride;
+        ra.gram_r = p->rbucket;
+    }
     if (ra.nmain + ra.nnorm > 0) PSGD_HIP(launch_reduce(ra, ra.nmain + ra.nnorm, s));
     return PSGD_OK;
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "psgd_internal.h"
 #include "psgd_stream.cuh"
@@ -949,6 +950,129 @@ struct CholNT {
 // RC = R: the panel has exactly R columns (compile-time rank: the r x r arithmetic is
 // branch-free straight-line fp64 that the compiler interleaves; it is a serial latency
 // chain per workgroup, so this matters); RC = 0: any r <= R at run time.
+// The r x r work of Cholesky-QR on one wave (a serial fp64 latency chain; the other waves
+// would only compete for the fp64 pipes): Cholesky of the Gram g (upper, NG entries), M =
+// R^-1, and LAPACK's column signs D from the top block T = X[0:r] M (`top`: the top R x R rows
+// in LDS, or null: loaded from st). Lane 0 publishes M D (m_sh, R x R), ok and R' = D R.
+template <int R>
+__device__ __forceinline__ void chol_chain(const double* g, const float* top, const float* st, int r, int64_t k,
+                                           double* m_sh, int* ok_sh, float* rfac) {
+        double Rm[R][R];
+        double inv[R];  // 1 / R_jj: one division per column, products elsewhere (the chain is
+                        // serial; each fp64 division is a ~10-instruction dependent sequence)
+        bool ok = true;
+        {
+            double G[R][R];
+            int e = 0;
+#pragma unroll
+            for (int c = 0; c < R; ++c)
+#pragma unroll
+                for (int b = c; b < R; ++b) {
+                    G[c][b] = g[e];
+                    G[b][c] = g[e];
+                    ++e;
+                }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+#pragma unroll
+                for (int b = 0; b < R; ++b) Rm[j][b] = 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                inv[j] = 1.0;
+                if (j < r) {
+                    double piv = G[j][j];
+#pragma unroll
+                    for (int l = 0; l < R; ++l)
+                        if (l < j) piv -= Rm[l][j] * Rm[l][j];
+                    ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
+                    const double d = sqrt(piv > 0.0 ? piv : 1.0);
+                    Rm[j][j] = d;
+                    inv[j] = 1.0 / d;
+#pragma unroll
+                    for (int b = 0; b < R; ++b)
+                        if (b > j && b < r) {
+                            double v = G[j][b];
+#pragma unroll
+                            for (int l = 0; l < R; ++l)
+                                if (l < j) v -= Rm[l][j] * Rm[l][b];
+                            Rm[j][b] = v * inv[j];
+                        }
+                }
+            }
+        }
+        // M = R^-1 (upper triangular, back substitution column by column)
+        double M[R][R];
+#pragma unroll
+        for (int c = 0; c < R; ++c) {
+#pragma unroll
+            for (int i = R - 1; i >= 0; --i) {
+                double v = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+                for (int l = 0; l < R; ++l)
+                    if (l > i && l < r) v -= Rm[i][l] * M[l][c];
+                M[i][c] = (i < r && c < r) ? v * inv[i] : 0.0;
+            }
+        }
+        // LAPACK column signs from the top block T = X[0:r] M
+        double T[R][R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            float x[R];
+            if (top) {
+#pragma unroll
+                for (int c = 0; c < R; ++c) x[c] = top[(i < r ? i : 0) * R + c];  // LDS, written before a barrier
+            } else {
+                ld_row<R>(st + int64_t(i < r ? i : 0) * r, r, x);
+            }
+#pragma unroll
+            for (int c = 0; c < R; ++c) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < R; ++l) v += double(x[l]) * M[l][c];
+                T[i][c] = v;
+            }
+        }
+        double sgn[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            if (j < r) {
+                const bool nonneg = T[j][j] >= 0.0;
+                // |T_jj| = 1 is LAPACK's xnorm == 0 column (tau = 0, beta = alpha, no flip):
+                // the reconstruction cannot tell it from a tiny trailing sub-column, so such
+                // panels (e.g. upper trapezoidal) take the exact Householder recursion
+                ok = ok && !(j < k - 1 && fabs(T[j][j]) > 1.0 - kSignTol);
+                sgn[j] = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
+                T[j][j] -= sgn[j];
+                const double ip = 1.0 / T[j][j];
+#pragma unroll
+                for (int i = 0; i < R; ++i)
+                    if (i > j && i < r) {
+                        const double l = T[i][j] * ip;
+#pragma unroll
+                        for (int b = 0; b < R; ++b)
+                            if (b > j && b < r) T[i][b] -= l * T[j][b];
+                    }
+            } else {
+                sgn[j] = 1.0;
+            }
+        }
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+#pragma unroll
+                for (int c = 0; c < R; ++c) m_sh[i * R + c] = M[i][c] * sgn[c];
+            *ok_sh = ok ? 1 : 0;
+            if (rfac && ok) {  // X = Q (D R): R' = D R
+#pragma unroll
+                for (int i = 0; i < R; ++i)
+#pragma unroll
+                    for (int c = 0; c < R; ++c)
+                        if (i < r && c < r) rfac[i * r + c] = i <= c ? float(sgn[i] * Rm[i][c]) : 0.f;
+            }
+        }
+}
+
 // Gram sums through LDS (NT x NG fp64 partials: 40 KB at rank 4) for r <= 4
 template <int R>
 constexpr bool kGramLds = R <= 4;
@@ -1031,127 +1155,10 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     }
     PSGD_STAMP(12);
 
-    // The r x r work (Cholesky, R^-1, LAPACK signs) is a serial fp64 latency chain: wave 0
-    // alone runs it (the other waves would only compete for the fp64 pipes) and publishes
-    // M = R^-1 D through LDS.
     __shared__ double m_sh[R * R];
     __shared__ int ok_sh;
-    if ((tid >> 6) == 0) {
-        double Rm[R][R];
-        double inv[R];  // 1 / R_jj: one division per column, products elsewhere (the chain is
-                        // serial; each fp64 division is a ~10-instruction dependent sequence)
-        bool ok = true;
-        {
-            double G[R][R];
-            int e = 0;
-#pragma unroll
-            for (int c = 0; c < R; ++c)
-#pragma unroll
-                for (int b = c; b < R; ++b) {
-                    G[c][b] = g[e];
-                    G[b][c] = g[e];
-                    ++e;
-                }
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-#pragma unroll
-                for (int b = 0; b < R; ++b) Rm[j][b] = 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                inv[j] = 1.0;
-                if (j < r) {
-                    double piv = G[j][j];
-#pragma unroll
-                    for (int l = 0; l < R; ++l)
-                        if (l < j) piv -= Rm[l][j] * Rm[l][j];
-                    ok = ok && piv > 1e-8 * G[j][j] && piv > 0.0;
-                    const double d = sqrt(piv > 0.0 ? piv : 1.0);
-                    Rm[j][j] = d;
-                    inv[j] = 1.0 / d;
-#pragma unroll
-                    for (int b = 0; b < R; ++b)
-                        if (b > j && b < r) {
-                            double v = G[j][b];
-#pragma unroll
-                            for (int l = 0; l < R; ++l)
-                                if (l < j) v -= Rm[l][j] * Rm[l][b];
-                            Rm[j][b] = v * inv[j];
-                        }
-                }
-            }
-        }
-        // M = R^-1 (upper triangular, back substitution column by column)
-        double M[R][R];
-#pragma unroll
-        for (int c = 0; c < R; ++c) {
-#pragma unroll
-            for (int i = R - 1; i >= 0; --i) {
-                double v = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-                for (int l = 0; l < R; ++l)
-                    if (l > i && l < r) v -= Rm[i][l] * M[l][c];
-                M[i][c] = (i < r && c < r) ? v * inv[i] : 0.0;
-            }
-        }
-        // LAPACK column signs from the top block T = X[0:r] M
-        double T[R][R];
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            float x[R];
-            if constexpr (kGramLds<R>) {
-#pragma unroll
-                for (int c = 0; c < R; ++c) x[c] = top_sh[(i < r ? i : 0) * R + c];  // written before the barrier
-            } else {
-                ld_row<R>(st + int64_t(i < r ? i : 0) * r, r, x);
-            }
-#pragma unroll
-            for (int c = 0; c < R; ++c) {
-                double v = 0.0;
-#pragma unroll
-                for (int l = 0; l < R; ++l) v += double(x[l]) * M[l][c];
-                T[i][c] = v;
-            }
-        }
-        double sgn[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-            if (j < r) {
-                const bool nonneg = T[j][j] >= 0.0;
-                // |T_jj| = 1 is LAPACK's xnorm == 0 column (tau = 0, beta = alpha, no flip):
-                // the reconstruction cannot tell it from a tiny trailing sub-column, so such
-                // panels (e.g. upper trapezoidal) take the exact Householder recursion
-                ok = ok && !(j < k - 1 && fabs(T[j][j]) > 1.0 - kSignTol);
-                sgn[j] = (j == k - 1) ? (nonneg ? 1.0 : -1.0) : (nonneg ? -1.0 : 1.0);
-                T[j][j] -= sgn[j];
-                const double ip = 1.0 / T[j][j];
-#pragma unroll
-                for (int i = 0; i < R; ++i)
-                    if (i > j && i < r) {
-                        const double l = T[i][j] * ip;
-#pragma unroll
-                        for (int b = 0; b < R; ++b)
-                            if (b > j && b < r) T[i][b] -= l * T[j][b];
-                    }
-            } else {
-                sgn[j] = 1.0;
-            }
-        }
-        if (tid == 0) {
-#pragma unroll
-            for (int i = 0; i < R; ++i)
-#pragma unroll
-                for (int c = 0; c < R; ++c) m_sh[i * R + c] = M[i][c] * sgn[c];
-            ok_sh = ok ? 1 : 0;
-            if (a.rfac && ok) {  // X = Q (D R): R' = D R
-#pragma unroll
-                for (int i = 0; i < R; ++i)
-#pragma unroll
-                    for (int c = 0; c < R; ++c)
-                        if (i < r && c < r) a.rfac[u.off + i * r + c] = i <= c ? float(sgn[i] * Rm[i][c]) : 0.f;
-            }
-        }
-    }
+    if ((tid >> 6) == 0) chol_chain<R>(g, kGramLds<R> ? top_sh : nullptr, st, r, k, m_sh, &ok_sh,
+                                       a.rfac ? a.rfac + u.off : nullptr);
     __syncthreads();
     PSGD_STAMP(13);
     if (!ok_sh) {  // exact Householder (geqr2 + org2r) in place in the history buffer
@@ -1499,6 +1506,102 @@ __device__ __forceinline__ void orth_chol_wide(const OrthArgs& a) {
 __global__ __launch_bounds__(kC16NT) void k_orth_chol16(OrthArgs a) { orth_chol_wide<16>(a); }
 __global__ __launch_bounds__(kC16NT) void k_orth_chol32(OrthArgs a) { orth_chol_wide<32>(a); }
 
+// ------------------------------------------- folded Cholesky-QR (projection form) ----
+// The Q panels of a two-iteration rank-2/4 step at world size 1: k_reduce left each item's
+// upper Gram (fp64) beside the reduced factor, so no pass over the panel forms it. Workgroup
+// (unit, slice) sums its unit's item partials (lane-strided in item order, then the wave
+// tree: fixed order, the same in every slice), runs k_orth_chol's chain (Cholesky, R^-1,
+// LAPACK signs from the top rows) and writes X = raw M D for its kChainRows rows (the same
+// fp64 row products as k_orth_chol's second pass): the panel is read once, spread over
+// ceil(k / kChainRows) CUs instead of one. A panel the chain rejects takes the exact
+// Householder recursion in slice 0 (the other slices return).
+template <int R>
+__global__ __launch_bounds__(CholNT<R>::value) void k_orth_chain(ChainArgs a) {
+    constexpr int NT = CholNT<R>::value;
+    constexpr int NG = R * (R + 1) / 2;
+    constexpr int kRows = 2;  // rows per thread: kChainRows = 2 NT
+    __shared__ double m_sh[R * R];
+    __shared__ int ok_sh;
+    __shared__ float top_sh[R * R];
+    __shared__ float red[NT / 64 * R];
+    __shared__ float tau[(R + 3) / 4 * 4];
+    const OrthUnit u = a.units[blockIdx.x];
+    const int r = R;  // the plan folds only panels of exactly R columns
+    const int64_t k = u.k;
+    const int64_t row0 = int64_t(blockIdx.y) * kRows * NT;
+    if (row0 >= k) return;  // uniform: short panels use fewer slices
+    const int tid = threadIdx.x, lane = tid & 63;
+    const float* raw = a.raw + u.off;
+    // this slice's rows go out first (in flight during the partial sums and the chain)
+    float x[kRows][R];
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) {
+        const int64_t i = row0 + tid + int64_t(q) * NT;
+        ld_row<R>(raw + (i < k ? i : 0) * r, r, x[q]);
+    }
+    if (tid < R * R) top_sh[tid] = raw[tid];  // the top R rows (k >= r)
+    double g[NG];
+    if (tid < 64) {
+        const int ib = a.uitems[2 * blockIdx.x], ie = a.uitems[2 * blockIdx.x + 1];
+#pragma unroll
+        for (int e = 0; e < NG; ++e) g[e] = 0.0;
+        for (int it0 = ib + lane; it0 < ie; it0 += 64) {
+#pragma unroll
+            for (int e = 0; e < NG; ++e) g[e] += a.gram[int64_t(it0) * kGramStride + e];
+        }
+#pragma unroll
+        for (int e = 0; e < NG; ++e) g[e] = wave_allsum_f64(g[e]);
+    }
+    __syncthreads();  // top_sh
+    if (tid < 64) chol_chain<R>(g, top_sh, raw, r, k, m_sh, &ok_sh, blockIdx.y == 0 ? a.rfac + u.off : nullptr);
+    __syncthreads();
+    float* st = a.state + u.off;
+    float* hx = a.hx + u.off;
+    if (!ok_sh) {
+        if (blockIdx.y != 0) return;
+        // exact Householder (geqr2 + org2r) in the history buffer, then the state
+        for (int64_t i = tid; i < k * r; i += NT) hx[i] = raw[i];
+        __syncthreads();
+        householder_q<R, NT>(hx, k, r, red, tau, a.rfac + u.off);
+        for (int64_t i = tid; i < k * r; i += NT) st[i] = hx[i];
+        return;
+    }
+    double M[R][R];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = 0; c < R; ++c) M[i][c] = m_sh[i * R + c];
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) {
+        const int64_t i = row0 + tid + int64_t(q) * NT;
+#pragma unroll
+        for (int c = 0; c < R; ++c) keep(x[q][c]);
+        float y[R];
+#pragma unroll
+        for (int c = 0; c < R; ++c) {
+            double v = 0.0;
+#pragma unroll
+            for (int l = 0; l < R; ++l) v += double(x[q][l]) * M[l][c];
+            y[c] = float(v);
+        }
+        if (i < k) {
+            st_row<R>(st + i * r, r, y);
+            st_row<R>(hx + i * r, r, y);
+        }
+    }
+}
+
+hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, int R, hipStream_t s) {
+    if (nunits == 0) return hipSuccess;
+    auto grid = [&](int nt) { return dim3(unsigned(nunits), unsigned((max_rows + 2 * nt - 1) / (2 * nt))); };
+    switch (R) {
+        case 2: k_orth_chain<2><<<grid(CholNT<2>::value), CholNT<2>::value, 0, s>>>(a); break;
+        case 4: k_orth_chain<4><<<grid(CholNT<4>::value), CholNT<4>::value, 0, s>>>(a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s) {
     switch (R) {
         case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
@@ -1733,9 +1836,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     }
     const int64_t dbase = a.even ? d.qoff : d.poff;
     float sq = 0.f;
+    float tv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        if (j >= per) break;
+        tv[j] = 0.f;
+        if (j >= per) continue;
         const int o = j * 64 + lane;
         float t = ((red[o] + red[kRedItem + o]) + red[2 * kRedItem + o]) + red[3 * kRedItem + o];
         if (nrm) t = t / nv;  // G^T (x / d) == (G^T x) / d up to rounding
@@ -1744,11 +1849,51 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
             a.yloc[dbase + e] = t;
             a.state[dbase + e] = t;
             sq = fmaf(t, t, sq);
+            tv[j] = t;
         }
     }
     if (a.ss_out) {  // this output is the next iteration's in-factor: its sum of squares
         const float v = wave_allsum(sq);
         if (lane == 0) a.ss_out[blockIdx.x] = v;
+    }
+    if (a.gram) {
+        // folded orthonormalisation: the upper Gram of this item's rows (r in {2, 4}; items
+        // start on a row and hold whole rows). The outputs go to LDS in element order (wave 0
+        // alone: its own earlier reads of `red` are ordered before these writes), then lane l
+        // takes rows l, l + 64, ...; fp64 products and sums, one fixed-order wave tree per entry.
+        const int r = a.gram_r, ng = r * (r + 1) / 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < per) red[vec ? 4 * lane + j : lane + 64 * j] = tv[j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int nrow = 64 * per / r;
+        double g[kGramStride];
+#pragma unroll
+        for (int e = 0; e < kGramStride; ++e) g[e] = 0.0;
+        auto rows = [&](auto RT) {  // compile-time r: register-indexed Gram entries
+            constexpr int RC = decltype(RT)::value;
+            for (int row = lane; row < nrow; row += 64) {
+                float x[RC];
+#pragma unroll
+                for (int c = 0; c < RC; ++c) x[c] = red[row * RC + c];
+                int e = 0;
+#pragma unroll
+                for (int c = 0; c < RC; ++c)
+#pragma unroll
+                    for (int b = c; b < RC; ++b) g[e++] += double(x[c]) * double(x[b]);
+            }
+        };
+        if (r == 4)
+            rows(std::integral_constant<int, 4>{});
+        else
+            rows(std::integral_constant<int, 2>{});
+#pragma unroll
+        for (int e = 0; e < kGramStride; ++e) {
+            if (e < ng) {
+                const double t = wave_allsum_f64(g[e]);
+                if (lane == 0) a.gram[int64_t(blockIdx.x) * kGramStride + e] = t;
+            }
+        }
     }
 }
 
