@@ -144,6 +144,42 @@ __device__ __forceinline__ void ld_factor(gptr<const float> p, int r, float (&v)
     }
 }
 
+// The same through the scalar data cache, for a wave-uniform row (s_load_dwordx4 / dwordx2 /
+// dword): read-only factor rows that every lane of a wave needs, kept off the vector memory
+// pipeline that streams the gradient.
+#define PSGD_C __attribute__((address_space(4)))
+template <int R>
+__device__ __forceinline__ void ld_factor_s(const float* base, int64_t off, int r, float (&v)[R]) {
+    const PSGD_C float* p = (const PSGD_C float*)(base) + off;
+    typedef float v4f_ __attribute__((ext_vector_type(4)));
+    typedef float v2f_ __attribute__((ext_vector_type(2)));
+    if constexpr (R == 1) {
+        v[0] = p[0];
+    } else if constexpr (R % 4 == 0) {
+        if (r == R) {
+#pragma unroll
+            for (int c = 0; c < R; c += 4) {
+                const v4f_ x = *(const PSGD_C v4f_*)(p + c);
+                v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < R; ++c) v[c] = c < r ? p[c] : 0.f;
+        }
+    } else if constexpr (R == 2) {
+        if (r == R) {
+            const v2f_ x = *(const PSGD_C v2f_*)p;
+            v[0] = x.x; v[1] = x.y;
+        } else {
+            v[0] = p[0];
+            v[1] = 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < R; ++c) v[c] = c < r ? p[c] : 0.f;
+    }
+}
+
 // sum_c a[c] * b[c] as an fma chain in c order (the order of a rank-r dot of one output
 // element in the reference's batched GEMM).
 template <int R>
@@ -295,6 +331,12 @@ constexpr int kUnroll = 4;  // rows in flight per lane
 #define PSGD_PROD_PIPE 0
 #endif
 constexpr int kProdUnroll = PSGD_PROD_UNROLL;
+// even product: wave-uniform in-factor rows through scalar loads (build-time knob for A/B;
+// measured slower at rank 4, 29.1 -> 32.4 us on ResNet-50, neutral at rank 1: off)
+#ifndef PSGD_PROD_SCALAR
+#define PSGD_PROD_SCALAR 0
+#endif
+constexpr bool kProdScalar = PSGD_PROD_SCALAR != 0;
 constexpr bool kProdPipe = PSGD_PROD_PIPE != 0;
 
 // ------------------------------------------------- odd product, row layout (VALU) --
@@ -526,7 +568,14 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 #pragma unroll
         for (int u = 0; u < kProdUnroll; ++u) {
             const int32_t prow = int32_t(b.rc[u]) * r;
-            if constexpr (EVEN) ld_factor<R>(xp_base + prow, r, b.xpu[u]);
+            if constexpr (EVEN) {
+                // full-width strips (64 lanes on one row): the row is wave-uniform, so its
+                // factor values come through the scalar cache (kProdScalar)
+                if (kProdScalar && g.L == 64)
+                    ld_factor_s<R>(a.x, d.poff + __builtin_amdgcn_readfirstlane(prow), r, b.xpu[u]);
+                else
+                    ld_factor<R>(xp_base + prow, r, b.xpu[u]);
+            }
             if constexpr (K > 0) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, b.apu[k][u]);
@@ -590,9 +639,12 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
         load(cur, g.first_row);
         for (int64_t row = g.first_row; row < g.row_end; row += step) {
             Batch nxt;
-            load(nxt, row + step);  // issued before cur is consumed (no keep(): that would wait)
+            // issued before cur is consumed (no keep(): that would wait); none past the chunk
+            // (wave-uniform: a tile's last batch prefetched nothing useful)
+            const bool more = row + step < g.row_end;
+            if (more) load(nxt, row + step);
             process(cur, row);
-            cur = nxt;
+            if (more) cur = nxt;
         }
     } else {
         for (int64_t row = g.first_row; row < g.row_end; row += step) {
