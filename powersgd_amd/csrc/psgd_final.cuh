@@ -139,7 +139,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     const int64_t row_end = d.n < row0 + d.fin_rows ? d.n : row0 + d.fin_rows;
     const int nres = K >= 0 ? K : a.nres;
     const uint32_t nbytes = uint32_t(d.n * d.m * int64_t(sizeof(T)));
-    const rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.grads[d.tensor], 0, int(nbytes), 0x00020000);
+    const rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.grads[t.tensor], 0, int(nbytes), 0x00020000);
     const rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(static_cast<T*>(a.out) + d.out_off, 0, int(nbytes),
                                                         0x00020000);
     const gptr<const float> X = gconst<float>(a.x) + d.qoff;

@@ -54,7 +54,9 @@ struct GroupDesc {
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
 struct Tile {
-    int32_t mat, strip, chunk, pad;
+    int32_t mat, strip, chunk;
+    int32_t tensor;  // fp32/bf16 streaming tiles: the matrix's gradient-table index (its pointer
+                     // load goes out beside the MatDesc load instead of after it)
 };
 
 // Reduction item for the partial-sum pass: 256 consecutive factor elements of one matrix.

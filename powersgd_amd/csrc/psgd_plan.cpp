@@ -555,15 +555,15 @@ struct psgd_plan {
             d.odd_mfma = (use_mfma && !valu && d.r <= 16 && span < (int64_t(1) << 31)) ? 1 : 0;
             for (int c = 0; c < g.nchunk; ++c)
                 for (int s = 0; s < g.nstrip; ++s) {
-                    tiles.push_back(Tile{int32_t(i), s, c, 0});
-                    if (!d.odd_mfma) tiles_ov.push_back(Tile{int32_t(i), s, c, 0});
+                    tiles.push_back(Tile{int32_t(i), s, c, d.tensor});
+                    if (!d.odd_mfma) tiles_ov.push_back(Tile{int32_t(i), s, c, d.tensor});
                 }
             if (d.odd_mfma) {
                 d.odd_sw = og.sw;
                 d.odd_chunk_rows = og.chunk_rows;
                 d.odd_nstrip = og.nstrip;
                 for (int c = 0; c < og.nchunk; ++c)
-                    for (int s = 0; s < og.nstrip; ++s) tiles_om.push_back(Tile{int32_t(i), s, c, 0});
+                    for (int s = 0; s < og.nstrip; ++s) tiles_om.push_back(Tile{int32_t(i), s, c, d.tensor});
             } else {
                 d.odd_sw = d.odd_chunk_rows = 0;
                 d.odd_nstrip = g.nstrip;
@@ -657,7 +657,7 @@ struct psgd_plan {
                 d.fin_S = fg.S;
                 d.fin_rows = fg.rows;
                 fin_smax = std::max(fin_smax, fg.S);
-                for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
+                for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), d.tensor});
             }
         }
         // Optional: largest tiles first (a greedy longest-processing-time order for the

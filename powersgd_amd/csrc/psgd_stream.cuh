@@ -428,7 +428,7 @@ __device__ __forceinline__ void odd_rows_tile(const ProductArgs& a, const MatDes
     const int32_t ccol = active ? col0 : 0;
     const int64_t row_begin = int64_t(t.chunk) * d.chunk_rows;
     const int64_t row_end = n < row_begin + d.chunk_rows ? n : row_begin + d.chunk_rows;
-    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
+    const gptr<const T> G = gconst<T>(a.grads[t.tensor]);
     const int nres = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;
 
@@ -519,7 +519,7 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                                              float* lds) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
-    const gptr<const T> G = gconst<T>(a.grads[d.tensor]);
+    const gptr<const T> G = gconst<T>(a.grads[t.tensor]);
     const int nres = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;  // register-cached terms
     const gptr<const float> xp_base = gconst<float>(a.x) + d.poff;
@@ -930,7 +930,7 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
     const int nrb = int((row_end - row0 - wave * 16 + kWaves * 16 - 1) / (kWaves * 16));  // >= 0
 
     const uint32_t nrec = uint32_t(((row_end - row0 - 1) * m + sw) * s);
-    const T* gbase = static_cast<const T*>(a.grads[d.tensor]) + row0 * m + j_begin;
+    const T* gbase = static_cast<const T*>(a.grads[t.tensor]) + row0 * m + j_begin;
     const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(gbase), 0, int(nrec), 0x00020000);
 
     float x[kOddSlots][4];
@@ -1131,7 +1131,7 @@ template <typename T, int R, int NI, bool SHARED, int V>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
-    const gptr<T> G = gmut<T>(a.grads[d.tensor]);
+    const gptr<T> G = gmut<T>(a.grads[t.tensor]);
     const gptr<T> D = a.rdst ? gmut<T>(a.rdst[d.tensor]) : G;  // residual destination
     const gptr<T> O = a.odst ? gmut<T>(a.odst[d.tensor]) : gmut<T>(a.out) + d.out_off;
     const int nt = NI > 0 ? NI : a.nterms;
