@@ -866,7 +866,11 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         // cold even product on ResNet-50 is fastest at 8k-element tiles (profiles/r02/tile_sweep.txt)
         int64_t total = 0;
         for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
-        const int64_t dflt = std::min<int64_t>(16384, std::max<int64_t>(4096, total / 3072));
+        // small plans (<= 4M elements): about one tile per CU (cfg5 4096 x 512: 8192-element
+        // tiles 0.038 -> 0.033 ms/step with the final blocks below; profiles/r02b/small)
+        const int64_t dflt = total <= (int64_t(1) << 22)
+                                 ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
+                                 : std::min<int64_t>(16384, std::max<int64_t>(4096, total / 3072));
         p->tile_elems = std::max<int64_t>(1024, env_int("PSGD_TILE_ELEMS", dflt));
     }
     if (maxr > 32) {
@@ -880,7 +884,9 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         // elements per block.
         int64_t total = 0;
         for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
-        const int64_t dflt = std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
+        const int64_t dflt = total <= (int64_t(1) << 22)
+                                 ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
+                                 : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
         // LDS form: one workgroup per CU that first loads the matrix's panels, so larger
         // blocks (~2 rounds over 256 CUs)
