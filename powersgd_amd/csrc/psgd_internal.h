@@ -136,7 +136,11 @@ struct ProductArgs {
     const int32_t* grng_in;
     const float* raw_in;
     float* xstate;
-    float* hx;
+    float* hx;    // even products, wave tiles (no fold): each wave of a workgroup takes its own tile
+    // (blockIdx * waves + wave of `ntiles`) and writes its partials from registers: no LDS
+    // reduction and no workgroup barrier in the epilogue
+    int32_t wave_tiles;
+    int32_t ntiles;
 };
 
 struct ApplyArgs {

@@ -1417,6 +1417,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     pa.nres = it;
     if (even) {
         const int nt = sp.tiles[1] - sp.tiles[0];
+        // wave tiles (opt-in A/B knob): no LDS reduction / barrier in the tile epilogue
+        static const bool wave_tiles = env_int("PSGD_PROD_WAVE", 0) != 0;
+        pa.wave_tiles = (wave_tiles && !fold) ? 1 : 0;
+        pa.ntiles = nt;
         if (nt > 0) PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, nt, s));
         if (fold) return PSGD_OK;  // the last tile of each strip reduced it
     } else {

@@ -337,6 +337,12 @@ constexpr int kProdUnroll = PSGD_PROD_UNROLL;
 #define PSGD_PROD_SCALAR 0
 #endif
 constexpr bool kProdScalar = PSGD_PROD_SCALAR != 0;
+// DIAGNOSTIC ONLY (timing ablations, wrong results): 1 = no in-factor row loads (constant 1),
+// 2 = no epilogue (no LDS reduction, no partial stores). Never set in a product build.
+#ifndef PSGD_PROD_ABL
+#define PSGD_PROD_ABL 0
+#endif
+constexpr int kProdAbl = PSGD_PROD_ABL;
 constexpr bool kProdPipe = PSGD_PROD_PIPE != 0;
 
 // ------------------------------------------------- odd product, row layout (VALU) --
@@ -514,10 +520,15 @@ __device__ __forceinline__ void odd_rows_tile(const ProductArgs& a, const MatDes
 }
 
 // ------------------------------------------------------------------ product -------
-template <typename T, int R, int K, bool EVEN, int V>
+template <typename T, int R, int K, bool EVEN, int V, bool WT = false>
 __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc& d, const Tile& t,
                                              float* lds) {
-    const TileGeom g = tile_geom<V>(d, t);
+    constexpr bool wt = WT;
+    TileGeom g = tile_geom<V>(d, t);
+    if constexpr (wt) {  // wave tile: this wave alone walks the chunk's rows
+        g.stride = 64 / g.L;
+        g.first_row = g.row_begin + g.sub;
+    }
     const int r = d.r;
     const gptr<const T> G = gconst<T>(a.grads[t.tensor]);
     const int nres = K >= 0 ? K : a.nres;
@@ -568,7 +579,10 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
 #pragma unroll
         for (int u = 0; u < kProdUnroll; ++u) {
             const int32_t prow = int32_t(b.rc[u]) * r;
-            if constexpr (EVEN) {
+            if constexpr (EVEN && (kProdAbl & 1)) {
+#pragma unroll
+                for (int c = 0; c < R; ++c) b.xpu[u][c] = 1.f;
+            } else if constexpr (EVEN) {
                 // full-width strips (64 lanes on one row): the row is wave-uniform, so its
                 // factor values come through the scalar cache (kProdScalar)
                 if (kProdScalar && g.L == 64)
@@ -634,7 +648,7 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
             }
         }
     };
-    if constexpr (kProdPipe) {
+    if constexpr (kProdPipe || (EVEN && wt)) {
         Batch cur;
         load(cur, g.first_row);
         for (int64_t row = g.first_row; row < g.row_end; row += step) {
@@ -657,7 +671,15 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
     if constexpr (EVEN && R == 1) {
         // iteration-0 norm fold: this chunk's share of the raw in-factor's sum of squares
         // (written before the partial reduction reuses the LDS scratch)
-        if (a.ss0 && t.strip == 0) {
+        if (WT && a.ss0 && t.strip == 0) {  // wave tile: one wave, no barrier
+            float sq = 0.f;
+            for (int64_t row = g.row_begin + g.lane; row < g.row_end; row += 64) {
+                const float x = xp_base[row];
+                sq = fmaf(x, x, sq);
+            }
+            sq = sum_within(sq, 64);
+            if (g.lane == 0) a.ss0[a.ss0_base[t.mat] + t.chunk] = sq;
+        } else if (a.ss0 && t.strip == 0) {
             float sq = 0.f;
             for (int64_t row = g.row_begin + threadIdx.x; row < g.row_end; row += kBlock) {
                 const float x = xp_base[row];
@@ -673,11 +695,42 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
             __syncthreads();
         }
     }
+    if constexpr (EVEN && (kProdAbl & 2)) {
+        float t = 0.f;
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int c = 0; c < R; ++c) t += acc[v][c];
+        if (t == 1234.5f) a.part[d.part_even] = t;  // keeps the loads alive
+        return;
+    }
     if constexpr (EVEN) {
 #pragma unroll
         for (int v = 0; v < V; ++v)
 #pragma unroll
             for (int c = 0; c < R; ++c) acc[v][c] = sum_across(acc[v][c], g.L);  // row phases
+        if constexpr (WT) {  // wave tile: the partials straight from registers (row-phase 0 lanes)
+            if (g.sub == 0) {
+                gptr<float> part = gmut<float>(a.part) + d.part_even + int64_t(t.chunk) * g.m * r;
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const int64_t col = int64_t(g.col0) + v;
+                    if (g.active && col < g.m) {
+                        if constexpr (R == 4) {
+                            if (r == 4) {
+                                const v4f x = {acc[v][0], acc[v][1], acc[v][2], acc[v][3]};
+                                *(gptr<v4f>)(part + col * 4) = x;
+                                continue;
+                            }
+                        }
+#pragma unroll
+                        for (int c = 0; c < R; ++c)
+                            if (c < r) part[col * r + c] = acc[v][c];
+                    }
+                }
+            }
+            return;
+        }
         const int width = g.L * V * R;  // floats per wave
         if (g.sub == 0) {
 #pragma unroll
@@ -687,16 +740,37 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
         }
         __syncthreads();
         gptr<float> part = gmut<float>(a.part) + d.part_even + int64_t(t.chunk) * g.m * r;
+        const int64_t col0 = int64_t(t.strip) * g.L * V;
+        // A full strip of an r == R matrix is one contiguous run of `width` partials: 16-byte
+        // plain stores of 4 consecutive sums per thread (the per-element order is unchanged).
+        // The dword write-through stores below cost the epilogue ~5 us per ResNet-50 rank-4
+        // product (one fabric write per dword; ablation in profiles/r02b/ab).
+        const bool vec_out = !a.fold && r == R && (width & 3) == 0 && col0 + g.L * V <= g.m &&
+                             ((d.part_even + int64_t(t.chunk) * g.m * r + col0 * R) & 3) == 0;
+        if (vec_out) {
+            gptr<float> dst = part + col0 * R;
+            for (int i4 = threadIdx.x * 4; i4 < width; i4 += kBlock * 4) {
+                v4f sv = *reinterpret_cast<const v4f*>(lds + i4);
+#pragma unroll
+                for (int w = 1; w < kWaves; ++w) sv += *reinterpret_cast<const v4f*>(lds + w * width + i4);
+                *(gptr<v4f>)(dst + i4) = sv;
+            }
+            return;
+        }
         for (int idx = threadIdx.x; idx < width; idx += kBlock) {
             float s = lds[idx];
 #pragma unroll
             for (int w = 1; w < kWaves; ++w) s += lds[w * width + idx];
             const int c = idx % R;
-            const int64_t col = int64_t(t.strip) * g.L * V + idx / R;
-            // write-through (sc1) stores: the folded reduction's last arriver on another XCD
-            // reads them after an acquire, with no release fence (and its L2 write-back) here
-            if (c < r && col < g.m)
-                __hip_atomic_store(&part[col * r + c], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t col = col0 + idx / R;
+            if (c < r && col < g.m) {
+                // folded reduction: write-through (sc1) stores, read by the last arriver on
+                // another XCD after an acquire, with no release fence (and L2 write-back) here
+                if (a.fold)
+                    __hip_atomic_store(&part[col * r + c], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    part[col * r + c] = s;
+            }
         }
     }
 }
@@ -819,11 +893,16 @@ __device__ __forceinline__ void fold_even_strip(const ProductArgs& a, const MatD
     }
 }
 
-template <typename T, int R, int K, bool EVEN>
+template <typename T, int R, int K, bool EVEN, bool WT = false>
 __global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
     // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees d.vec == 0)
-    __shared__ float lds[EVEN ? kWaves * 64 * (R <= 8 ? 4 : 1) * R : 1];
-    const Tile t = a.tiles[blockIdx.x];
+    __shared__ float lds[EVEN && !WT ? kWaves * 64 * (R <= 8 ? 4 : 1) * R : 1];
+    int tix = blockIdx.x;
+    if constexpr (WT) {  // wave tiles (even, no fold): wave-uniform exit, no barrier follows
+        tix = int(blockIdx.x) * kWaves + int(threadIdx.x >> 6);
+        if (tix >= a.ntiles) return;
+    }
+    const Tile t = a.tiles[tix];
     const MatDesc d = a.mats[t.mat];
     if constexpr (!EVEN && R <= 4) {
         if (d.vec && d.lanes == 64) {  // full-width strips: row layout + reduce-scatter
@@ -833,14 +912,14 @@ __global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
     }
     if constexpr (R <= 8) {
         if (d.vec) {
-            product_tile<T, R, K, EVEN, 4>(a, d, t, lds);
+            product_tile<T, R, K, EVEN, 4, WT>(a, d, t, lds);
             if constexpr (EVEN) {
                 if (a.fold) fold_even_strip(a, d, t, lds);
             }
             return;
         }
     }
-    product_tile<T, R, K, EVEN, 1>(a, d, t, lds);
+    product_tile<T, R, K, EVEN, 1, WT>(a, d, t, lds);
     if constexpr (EVEN) {
         if (a.fold) fold_even_strip(a, d, t, lds);
     }
@@ -1259,12 +1338,16 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
 // ------------------------------------------------------------------ dispatch ------
 template <typename T, int R>
 hipError_t dispatch_product_r(bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
-    const dim3 grid(ntiles), block(kBlock);
     constexpr bool kCache = R <= 8;
     const int K = (kCache && nres <= 3) ? nres : -1;
+    // wave tiles only for the register-cached instances (ranks <= 8, <= 3 terms)
+    const bool wtl = even && a.wave_tiles && K >= 0;
+    const dim3 grid(wtl ? (ntiles + kWaves - 1) / kWaves : ntiles), block(kBlock);
 #define PSGD_P(KK)                                                                       \
     do {                                                                                 \
-        if (even)                                                                        \
+        if (even && a.wave_tiles && KK >= 0)                                             \
+            k_product<T, R, (KK >= 0 ? KK : 0), true, true><<<grid, block, 0, s>>>(a);   \
+        else if (even)                                                                   \
             k_product<T, R, KK, true><<<grid, block, 0, s>>>(a);                         \
         else                                                                             \
             k_product<T, R, KK, false><<<grid, block, 0, s>>>(a);                        \
