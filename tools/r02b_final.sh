@@ -2,7 +2,7 @@
 # round-2 closing measurements (second session): GPU suite (+ parity log), smoke, default bench,
 # every config, cold kernel traces + PMC traffic for cfg2 and cfg3. Output under gpurun_out/final2/.
 set -o pipefail
-O=gpurun_out/final2; mkdir -p $O
+O=${OUT:-gpurun_out/final2}; mkdir -p $O
 export PSGD_PARITY_LOG=$O/parity_errors.jsonl
 rm -f $PSGD_PARITY_LOG
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -20 $O/pytest_gpu.log; exit 1; }
