@@ -587,7 +587,7 @@ __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
 // Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
 // CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
 template <typename T, int R, int SMAX>
-__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : 1))) void k_final_proj(
+__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 && SMAX < 5 ? 4 : 1))) void k_final_proj(
     FinalArgs a) {
     final_odd_block<T, R, 0, SMAX, true>(a);
 }
@@ -727,6 +727,9 @@ template <typename T, int R>
 hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s, waves);
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
+    if constexpr (R == 4) {  // projection form only: 5 segments at 2 waves per SIMD (PSGD_PROJ_S5)
+        if (smax <= 5 && nres == kFinProj) return launch_final_k<T, 4, 5, 0, true>(a, ntiles, s, waves);
+    }
     if constexpr (R <= 2) {
         if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
         if (smax <= 12 && nres <= 1) {

@@ -346,6 +346,7 @@ struct psgd_plan {
     size_t o_cnt = 0, o_gcnt = 0, o_ss_strip = 0, o_grng_strip = 0, o_gdesc = 0;
     bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
     bool fin_proj = false;       // ... in its projection form (I = 2, psgd_aggregate only)
+    bool proj_s5 = false;        // the projection form with 5-segment row groups (rank 4, opt-in)
     int fin_smax = 0;
     int fin_lds_bytes = 0;
     int64_t fin_elems = 32768, fin_elems_lds = 65536, tiles_fin_cap = 0;
@@ -638,6 +639,13 @@ struct psgd_plan {
                        launch_final_odd(dtype, rbucket, kFinProj, fin_bucket(smax), none, 0, nullptr, &waves) ==
                            hipSuccess &&
                        waves >= 2;
+            // opt-in: rank 4 with up to 5 register segments (fewer idle lanes on 9c-column rows,
+            // 2 waves per SIMD); only when no K-term fused form shares the tile list
+            proj_s5 = false;
+            if (fin_proj && !fin_ok && rbucket == 4 && env_int("PSGD_PROJ_S5", 0) != 0) {
+                int w5 = 0;
+                proj_s5 = launch_final_odd(dtype, 4, kFinProj, 5, none, 0, nullptr, &w5) == hipSuccess && w5 >= 2;
+            }
         }
         fin_smax = 0;
         if (fin_ok || fin_proj) {
@@ -648,7 +656,7 @@ struct psgd_plan {
             int scap = 0;
             if (env_int("PSGD_FIN_GEOM", 1) && !fin_lds) {
                 for (const MatDesc& d : mats) scap = std::max(scap, fin_geometry(d.n, d.m, f, 0).S);
-                scap = std::min(fin_bucket(scap), 5);
+                scap = proj_s5 ? 5 : std::min(fin_bucket(scap), 5);
             }
             for (size_t i = 0; i < mats.size(); ++i) {
                 MatDesc& d = mats[i];
