@@ -259,10 +259,12 @@ def main():
         total_ms, launches = codec._plan.timing_read()
         codec._plan.set_timing(False)
         codec.overlap = was
-        return total_ms / max(launches, 1), first
+        # per STEP: at world size > 1 the final pass is one launch per collective bucket, and
+        # the algorithmic bytes below are the whole step's final pass
+        return total_ms / a.steps, first, launches / a.steps
 
-    apply_ms_cold, first_cold = kernel_pass(lambda k: k % S) if do_cold else (None, None)
-    apply_ms_warm, first_warm = kernel_pass(lambda k: 0) if do_warm else (None, None)
+    apply_ms_cold, first_cold, lps_cold = kernel_pass(lambda k: k % S) if do_cold else (None, None, None)
+    apply_ms_warm, first_warm, lps_warm = kernel_pass(lambda k: 0) if do_warm else (None, None, None)
     if first_cold is None:
         first_cold = first_warm
 
@@ -281,11 +283,13 @@ def main():
           "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")"))
     kname = kf if nf == a.steps else "k_apply (fused residual + output)" if nf == 0 else f"{kf} / k_apply, alternating"
 
-    def roof(apply_ms, cache):
+    def roof(apply_ms, cache, lps):
         ach = ab / (apply_ms * 1e-3) / 1e9
         return {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(a.config, cache),
-                "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2), "cache": cache}
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": load_pmc_traffic(a.config, cache) if world == 1 else None,
+                "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2),
+                "launches_per_step": round(lps, 2), "cache": cache}
 
     def step_roof(elapsed):
         ms = elapsed / a.steps * 1e3
@@ -318,13 +322,13 @@ def main():
                    "buckets": len(codec._buckets) if codec._buckets else 1,
                    "backend": (backend if world > 1 else None)},
         "per_rank_GBs": round(value / world, 3),
-        "roofline": roof(apply_ms_cold, "cold") if do_cold else roof(apply_ms_warm, "warm"),
+        "roofline": roof(apply_ms_cold, "cold", lps_cold) if do_cold else roof(apply_ms_warm, "warm", lps_warm),
         "step_roofline": step_roof(head),
     }
     if do_cold and do_warm:
         out["warm"] = {"value": round(world * grad_bytes * a.steps / warm / 1e9, 3),
                        "ms_per_step": round(warm / a.steps * 1e3, 4),
-                       "roofline": roof(apply_ms_warm, "warm"), "step_roofline": step_roof(warm)}
+                       "roofline": roof(apply_ms_warm, "warm", lps_warm), "step_roofline": step_roof(warm)}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
     elif rank == 0:
