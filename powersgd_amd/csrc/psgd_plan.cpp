@@ -203,6 +203,8 @@ FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int sca
 }
 
 int fin_bucket(int s) { return s <= 2 ? 2 : s <= 3 ? 3 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
+// widest register-segment instance of the K-term final kernels per rank bucket (psgd_final.cuh)
+int fin_smax_inst(int R) { return R <= 2 ? 5 : 3; }
 
 // Device-resident pointer tables (gradients, destinations) without a host synchronisation.
 // kSlots tables live in the caller's workspace; a call whose pointer set matches a slot uses
@@ -657,6 +659,8 @@ struct psgd_plan {
             if (env_int("PSGD_FIN_GEOM", 1) && !fin_lds) {
                 for (const MatDesc& d : mats) scap = std::max(scap, fin_geometry(d.n, d.m, f, 0).S);
                 scap = proj_s5 ? 5 : std::min(fin_bucket(scap), 5);
+                if (const int64_t sc = env_int("PSGD_FIN_SCAP", 0))  // A/B knob: segment cap
+                    scap = int(std::min<int64_t>(sc, fin_smax_inst(rbucket)));
             }
             for (size_t i = 0; i < mats.size(); ++i) {
                 MatDesc& d = mats[i];
