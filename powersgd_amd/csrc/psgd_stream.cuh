@@ -893,8 +893,12 @@ __device__ __forceinline__ void fold_even_strip(const ProductArgs& a, const MatD
     }
 }
 
+// PSGD_PROD_WPE (A/B build knob): an occupancy target (waves per SIMD) for the even product
+#ifndef PSGD_PROD_WPE
+#define PSGD_PROD_WPE 1
+#endif
 template <typename T, int R, int K, bool EVEN, bool WT = false>
-__global__ __launch_bounds__(kBlock) void k_product(ProductArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EVEN && !WT ? PSGD_PROD_WPE : 1))) void k_product(ProductArgs a) {
     // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees d.vec == 0)
     __shared__ float lds[EVEN && !WT ? kWaves * 64 * (R <= 8 ? 4 : 1) * R : 1];
     int tix = blockIdx.x;
