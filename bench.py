@@ -247,10 +247,6 @@ def main():
     # roofline passes: the same K steps again with HIP events around every final-pass launch,
     # recorded by the library on the launch stream
     def kernel_pass(pick):
-        # the kernels alone: at world size 1 the bucket overlap (two side streams) would make
-        # the event-bracketed durations of concurrent launches overlap, so it is off here
-        was = codec._overlap_on
-        codec.overlap = False
         codec._plan.set_timing(True)
         first = codec.step_counter
         for k in range(a.steps):
@@ -258,7 +254,6 @@ def main():
         torch.cuda.synchronize()
         total_ms, launches = codec._plan.timing_read()
         codec._plan.set_timing(False)
-        codec.overlap = was
         # per STEP: at world size > 1 the final pass is one launch per collective bucket, and
         # the algorithmic bytes below are the whole step's final pass
         return total_ms / a.steps, first, launches / a.steps
@@ -317,8 +312,6 @@ def main():
                    "compressed_tensors": sum(mask), "gradient_bytes_per_rank": grad_bytes,
                    "parallelism": f"dp{world}", "cache": "cold" if do_cold else "warm",
                    "gradient_sets": S if do_cold else 1,
-                   "w1_bucket_overlap": bool(world == 1 and codec.overlap),
-                   "hip_graphs": bool(world == 1 and codec._graphs),
                    "buckets": len(codec._buckets) if codec._buckets else 1,
                    "backend": (backend if world > 1 else None)},
         "per_rank_GBs": round(value / world, 3),

@@ -137,7 +137,8 @@ int psgd_decompress(psgd_plan* plan, void* const* grads, void* out, int64_t step
  * buffer (psgd_plan_bucket_range: element offset/length in the P and Q state buffers) as soon
  * as bucket b's kernels are queued, so that collective overlaps the next buckets' kernels. The
  * element-wise SUM over the slices equals the whole-buffer SUM. nbuckets = 0: one bucket (the
- * whole plan). Synchronous (rewrites the tile tables): call between steps. fp32/bf16 plans. */
+ * whole plan); at most 8 buckets. Synchronous (rewrites the tile tables): call between steps.
+ * fp32/bf16 plans. */
 int psgd_plan_set_buckets(psgd_plan* plan, int32_t nbuckets, const int32_t* group_end);
 int psgd_plan_bucket_range(const psgd_plan* plan, int32_t bucket, int64_t* p_off, int64_t* p_len,
                            int64_t* q_off, int64_t* q_len);
@@ -146,23 +147,6 @@ int psgd_compress_bucket(psgd_plan* plan, void* const* grads, int64_t step, int3
                          void* stream);
 int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64_t step,
                            int32_t world_size, int32_t bucket, void* stream);
-
-/* World size 1 with buckets: the buckets are independent sub-steps (whole shape groups), so
- * they may run on different streams, where one bucket's latency-bound launches (reduction,
- * orthonormalisation) overlap another bucket's streaming passes. psgd_plan_prepare selects the
- * gradient pointer table on `stream` (call it on the stream the buckets' streams wait on, before
- * forking); psgd_aggregate_bucket = psgd_aggregate_flat restricted to one bucket (pass the flat
- * plan with exactly one of the buckets, or none). */
-int psgd_plan_prepare(psgd_plan* plan, void* const* grads, void* stream);
-/* World-size-1 execution of psgd_aggregate / psgd_aggregate_flat (both default off: measured
- * slower than plain launches on MI355X with ROCm 7.2). graphs != 0: each distinct
- * (pointer-table slot, output pointers, parity class) step is captured once as a HIP graph and
- * replayed with one launch (plan-owned stream, event-ordered after `stream`); off while timing is
- * on. overlap != 0: with buckets set, the buckets run as independent sub-steps on two plan-owned
- * side streams (inside the graph when graphs are on). */
-int psgd_plan_set_graphs(psgd_plan* plan, int32_t graphs, int32_t overlap);
-int psgd_aggregate_bucket(psgd_plan* plan, void* const* grads, void* out, int64_t step, int32_t bucket,
-                          psgd_flat* flat, void* const* unc, void* flat_out, void* stream);
 
 /* ----------------------------- one-shot all-reduce of the last factor over IPC (W > 1) ------ */
 /* Single node, one process per GPU: instead of a ring all-reduce of the last iteration's

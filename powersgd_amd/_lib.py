@@ -53,9 +53,6 @@ _SIGNATURES = {
     "psgd_plan_bucket_range": ([_vp, _i32, _P_i64, _P_i64, _P_i64, _P_i64], _i32),
     "psgd_compress_bucket": ([_vp, _vp, _i64, _i32, _i32, _vp], _i32),
     "psgd_decompress_bucket": ([_vp, _vp, _vp, _i64, _i32, _i32, _vp], _i32),
-    "psgd_plan_prepare": ([_vp, _vp, _vp], _i32),
-    "psgd_plan_set_graphs": ([_vp, _i32, _i32], _i32),
-    "psgd_aggregate_bucket": ([_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp], _i32),
     "psgd_ipc_handle_bytes": ([_P_i64], _i32),
     "psgd_ipc_create": ([_vp, _vp], _i32),
     "psgd_ipc_open": ([_vp, _i32, _i32, _vp], _i32),
@@ -207,17 +204,6 @@ class Plan:
 
     def decompress_bucket(self, grads, out_ptr: int, step: int, world: int, bucket: int, stream: int) -> None:
         check(lib().psgd_decompress_bucket(self._h, grads, out_ptr, step, world, bucket, stream))
-
-    def set_graphs(self, graphs: bool, overlap: bool) -> None:
-        check(lib().psgd_plan_set_graphs(self._h, 1 if graphs else 0, 1 if overlap else 0))
-
-    def prepare(self, grads, stream: int) -> None:
-        check(lib().psgd_plan_prepare(self._h, grads, stream))
-
-    def aggregate_bucket(self, grads, out_ptr: int, step: int, bucket: int, flat, unc, flat_out: int,
-                         stream: int) -> None:
-        check(lib().psgd_aggregate_bucket(self._h, grads, out_ptr, step, bucket, flat._h if flat else None, unc,
-                                          flat_out, stream))
 
     # --- one-shot all-reduce of the last factor over IPC mappings (W > 1, one node)
     def ipc_create(self) -> bytes:

@@ -1,0 +1,447 @@
+// k_even — the even power iteration's product Q = G_k^T X (reference powersgd.py:185-193, with
+// the error feedback of :195-202 formed on the fly), as a PERSISTENT streaming pass (gfx950).
+//
+// The plan cuts the gradient bytes of all matrices (or of one bucket of shape groups) into
+// equal ranges, one per workgroup, walking matrices -> column strips -> rows. A range is a short
+// list of segments (Seg: rows [row0, row1) of one strip); a strip is cut only where a
+// workgroup's range ends. Inside a segment every lane OWNS V consecutive columns (V = 4: 16-byte
+// fp32 / 8-byte bf16 loads) and the NW waves x (64 / L) row phases walk the rows, kEvenU rows in
+// flight per lane; the factor rows X[i, :] travel with the gradient rows. At the end of a
+// segment the row phases are summed (DPP inside a wave, then the waves in index order through
+// LDS) into ONE column partial per segment: the partial slab is (workgroups + strips) x strip
+// width x r floats instead of one per small tile, and k_reduce sums a handful of partials per
+// element, always in the same order (bitwise reproducible, no float atomics).
+//
+// Against the tile grid it replaces (13k short-lived waves of ~8 KB each, 63 % of wave time
+// parked in s_waitcnt/barrier, 13 MB of rank-4 partials), the persistent form keeps every
+// wave streaming the same strip for hundreds of rows and pays the tile epilogue once per
+// segment (a few per workgroup).
+#pragma once
+
+#include "psgd_stream.cuh"
+
+namespace psgd {
+
+// Threads per workgroup and gradient rows in flight per lane (build-time knobs for A/B runs).
+// The plan launches PSGD_EVEN_WPC (default 4) workgroups per CU, fewer on small plans (at least
+// PSGD_EVEN_MIN gradient elements each).
+#ifndef PSGD_EVEN_NT
+#define PSGD_EVEN_NT 512
+#endif
+#ifndef PSGD_EVEN_U
+#define PSGD_EVEN_U 4
+#endif
+constexpr int kEvenNT = PSGD_EVEN_NT;
+constexpr int kEvenNW = kEvenNT / 64;
+constexpr int kEvenU = PSGD_EVEN_U;
+
+// Wave-uniform copies (v_readfirstlane): LLVM cannot prove that threadIdx.x >> 6 or a value
+// loaded from a uniform address is the same in every lane, and keeps them in VGPRs, which turns
+// buffer-descriptor loads into waterfall loops and the in-factor rows into vector loads.
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int32_t(uint32_t(x))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int32_t(uint32_t(uint64_t(x) >> 32))));
+    return int64_t((uint64_t(hi) << 32) | lo);
+}
+__device__ __forceinline__ const void* uni(const void* p) {
+    return reinterpret_cast<const void*>(uni(int64_t(reinterpret_cast<uintptr_t>(p))));
+}
+__device__ __forceinline__ Seg uni(const Seg& s) {
+    Seg u;
+    u.m = uni(s.m);
+    u.poff = uni(s.poff);
+    u.qoff = uni(s.qoff);
+    u.part = uni(s.part);
+    u.row0 = uni(s.row0);
+    u.row1 = uni(s.row1);
+    u.strip = uni(s.strip);
+    u.tensor = uni(s.tensor);
+    u.ss = uni(s.ss);
+    u.r = uni(s.r);
+    u.lanes = uni(s.lanes);
+    u.vec = uni(s.vec);
+    return u;
+}
+
+// End of a segment: the rank-1 norm fold's share of sum_rows X^2 (strip-0 segments), the row
+// phases summed (DPP inside a wave, then the waves in index order through LDS) and ONE partial
+// [strip columns][r] stored at sg.part (r == R: one contiguous run, 16-byte stores).
+template <int R, int V>
+__device__ __forceinline__ void even_epilogue(const ProductArgs& a, const Seg& sg, int L, float (&acc)[V][R],
+                                              float* red, float* ssl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane / L, ql = lane - sub * L;
+    const int r = sg.r;
+    const int64_t m = sg.m;
+    const int64_t rb = sg.row0, re = sg.row1;
+    // rank-1 iteration 0 with the norm folded: this strip-0 segment's share of the RAW
+    // in-factor's sum of squares (rows in a fixed lane-strided order, then waves in order)
+    if constexpr (R == 1) {
+        if (a.ss0 && sg.ss >= 0) {
+            const float* xp = a.x + sg.poff;
+            float sq = 0.f;
+            for (int64_t row = rb + tid; row < re; row += kEvenNT) {
+                const float v = xp[row];
+                sq = fmaf(v, v, sq);
+            }
+            sq = wave_allsum(sq);
+            if (lane == 0) ssl[wave] = sq;
+        }
+    }
+    // row phases inside the wave, then the waves in index order
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int c = 0; c < R; ++c) acc[v][c] = sum_across(acc[v][c], L);
+    const int width = L * V * R;  // floats per wave: the strip's columns x R
+    if (sub == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int c = 0; c < R; ++c) red[wave * width + (ql * V + v) * R + c] = acc[v][c];
+    }
+    __syncthreads();
+    if constexpr (R == 1) {
+        if (a.ss0 && sg.ss >= 0 && tid == 0) {
+            float tot = ssl[0];
+#pragma unroll
+            for (int w = 1; w < kEvenNW; ++w) tot += ssl[w];
+            a.ss0[sg.ss] = tot;
+        }
+    }
+    // partial of this segment: [strip column][r] at sg.part (r == R: one contiguous run, 16-byte
+    // stores of 4 consecutive sums)
+    gptr<float> part = gmut<float>(a.part) + sg.part;
+    const int64_t cbase = int64_t(sg.strip) * L * V;
+    if (r == R && (width & 3) == 0 && cbase + L * V <= m && (sg.part & 3) == 0) {
+        for (int i4 = tid * 4; i4 < width; i4 += kEvenNT * 4) {
+            v4f s = *reinterpret_cast<const v4f*>(red + i4);
+#pragma unroll
+            for (int w = 1; w < kEvenNW; ++w) s += *reinterpret_cast<const v4f*>(red + w * width + i4);
+            *(gptr<v4f>)(part + i4) = s;
+        }
+    } else {
+        for (int idx = tid; idx < width; idx += kEvenNT) {
+            float s = red[idx];
+#pragma unroll
+            for (int w = 1; w < kEvenNW; ++w) s += red[w * width + idx];
+            const int c = idx % R;
+            const int64_t jc = idx / R;
+            if (c < r && cbase + jc < m) part[jc * r + c] = s;
+        }
+    }
+    __syncthreads();  // `red` is written again by the next segment
+}
+
+// A wave-uniform row of R factor values through the scalar data cache (s_load_dwordx1/2/4/8):
+// the in-factor rows of a full-width strip are the same for all 64 lanes, so they cost SGPRs
+// (used directly as FMA operands), not VGPRs or vector-memory slots.
+#define PSGD_C __attribute__((address_space(4)))
+template <int R>
+__device__ __forceinline__ void ld_row_s(const float* base, int64_t off, float (&v)[R]) {
+    const PSGD_C float* p = (const PSGD_C float*)(base) + off;
+    if constexpr (R == 1) {
+        v[0] = p[0];
+    } else if constexpr (R == 2) {
+        const v2f x = *(const PSGD_C v2f*)p;
+        v[0] = x.x;
+        v[1] = x.y;
+    } else {
+#pragma unroll
+        for (int c = 0; c < R; c += 4) {
+            const v4f x = *(const PSGD_C v4f*)(p + c);
+            v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
+        }
+    }
+}
+
+// Full-width strip (256 columns: 64 lanes x 4, r == R): every row a wave touches is
+// wave-uniform, so the in-factor rows come through the scalar cache, and the gradient rows
+// through a buffer descriptor spanning the segment's rows (rows past the segment and columns
+// past the matrix load 0 without a clamp or a branch). 32-bit offsets from the segment's first
+// row; the loop state is scalar. Same arithmetic order as even_seg.
+template <typename T, int R, int K>
+__device__ __forceinline__ void even_seg_full(const ProductArgs& a, const Seg& sg, const void* gp, float* red,
+                                              float* ssl) {
+    constexpr uint32_t s = sizeof(T);
+    constexpr int U = kEvenU;
+    const int lane = threadIdx.x & 63, wave = uni(int32_t(threadIdx.x >> 6));
+    const int32_t m = int32_t(sg.m);
+    const int32_t col0 = sg.strip * 256 + 4 * lane;
+    const bool active = col0 < m;
+    const int32_t rb = sg.row0, re = sg.row1;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(static_cast<const T*>(gp) + int64_t(rb) * m), 0, int(uint32_t(re - rb) * uint32_t(m) * s),
+        0x00020000);
+    const uint32_t cofs = active ? uint32_t(col0) * s : kOob;
+    const uint32_t rstride = uint32_t(m) * s;  // bytes per row
+    const float* xb = a.x + sg.poff;
+    constexpr int KC = K > 0 ? K : 1;
+    const int nres = K >= 0 ? K : a.nres;
+    float bq[KC][4][R];  // Q_k values of this lane's columns
+    if constexpr (K > 0) {
+        const int32_t cc = active ? col0 : 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) ld_factor<R>(gconst<float>(a.res.q[k]) + sg.qoff + (cc + v) * R, R, bq[k][v]);
+    }
+    float acc[4][R];
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int c = 0; c < R; ++c) acc[v][c] = 0.f;
+
+    for (int32_t row = rb + wave; row < re; row += U * kEvenNW) {
+        float x[U][4];
+        float xs[U][R];
+        float ap[KC][U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            BufIo<T>::ld4(rs, uint32_t(row + u * kEvenNW - rb) * rstride + cofs, x[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t ru = row + u * kEvenNW;
+            const int32_t xr = ru < re ? ru : rb;  // clamped (the gradient row loads 0)
+            ld_row_s<R>(xb, int64_t(xr) * R, xs[u]);
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) ld_row_s<R>(a.res.p[k] + sg.poff, int64_t(xr) * R, ap[k][u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) keep(x[u][v]);
+            if constexpr (K != 0) {
+                // error feedback of the earlier iterations (reference :195-202), element by element;
+                // rows past the segment and inactive columns must stay 0 afterwards
+                const int32_t ru = row + u * kEvenNW;
+                const int32_t xr = ru < re ? ru : rb;
+                const bool valid = active && ru < re;
+                for (int k = 0; k < nres; ++k) {
+                    float pk[R];
+                    if constexpr (K > 0) {
+#pragma unroll
+                        for (int c = 0; c < R; ++c) pk[c] = ap[k < KC ? k : 0][u][c];
+                    } else {
+                        ld_row_s<R>(a.res.p[k] + sg.poff, int64_t(xr) * R, pk);
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        float qk[R];
+                        if constexpr (K > 0) {
+#pragma unroll
+                            for (int c = 0; c < R; ++c) qk[c] = bq[k < KC ? k : 0][v][c];
+                        } else {
+                            const int32_t cc = active ? col0 : 0;
+                            ld_factor<R>(gconst<float>(a.res.q[k]) + sg.qoff + (cc + v) * R, R, qk);
+                        }
+                        x[u][v] = x[u][v] - dotr<R>(pk, qk);
+                    }
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) x[u][v] = valid ? x[u][v] : 0.f;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) acc[v][c] = fmaf(x[u][v], xs[u][c], acc[v][c]);
+        }
+    }
+    even_epilogue<R, 4>(a, sg, 64, acc, red, ssl);
+}
+
+template <typename T, int R, int K, int V>
+__device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, const void* gp, float* red,
+                                         float* ssl) {
+    constexpr uint32_t s = sizeof(T);
+    constexpr int U = R <= 8 ? kEvenU : R == 16 ? 2 : 1;  // fewer rows in flight at ranks 16/32
+    const int tid = threadIdx.x, lane = tid & 63, wave = uni(int32_t(tid >> 6));
+    const int L = sg.lanes, rw = 64 / L;
+    const int sub = lane / L, ql = lane - sub * L;
+    const int r = sg.r;
+    const int32_t m = int32_t(sg.m);
+    const int32_t col0 = (sg.strip * L + ql) * V;
+    const bool active = col0 < m;  // V == 4 only when m % 4 == 0: the whole vector is in range
+    const int32_t ccol = active ? col0 : 0;
+    const int32_t rb = sg.row0, re = sg.row1;
+    const int stride = kEvenNW * rw;
+    // gradient rows through a buffer descriptor spanning the segment's rows (rows past it and
+    // columns past the matrix load 0); 32-bit offsets from the segment's first row
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(static_cast<const T*>(gp) + int64_t(rb) * m), 0, int(uint32_t(re - rb) * uint32_t(m) * s),
+        0x00020000);
+    const uint32_t rstride = uint32_t(m) * s;
+    const gptr<const float> xp = gconst<float>(a.x) + sg.poff;
+    const int nres = K >= 0 ? K : a.nres;
+    constexpr int KC = K > 0 ? K : 1;  // register-cached error-feedback terms
+
+    float bq[KC][V][R];  // Q_k values of this lane's columns (constant over the segment)
+    if constexpr (K > 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int v = 0; v < V; ++v) ld_factor<R>(gconst<float>(a.res.q[k]) + sg.qoff + (ccol + v) * r, r, bq[k][v]);
+    }
+    float acc[V][R];
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int c = 0; c < R; ++c) acc[v][c] = 0.f;
+
+    for (int32_t row = rb + wave * rw + sub; row < re + sub; row += U * stride) {
+        float x[U][V];
+        float xr[U][R];
+        float ap[KC][U][R];
+        // every load of the batch is issued before any is consumed (no exec-mask branch per
+        // load: rows past the segment are out of the descriptor's range and load 0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t off = active ? uint32_t(row + u * stride - rb) * rstride + uint32_t(col0) * s : kOob;
+            if constexpr (V == 4) {
+                BufIo<T>::ld4(rs, off, x[u]);
+            } else {
+                x[u][0] = BufIo<T>::ld1(rs, off);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t ru = row + u * stride;
+            const int32_t xi = ru < re ? ru : rb;  // clamped factor row
+            ld_factor<R>(xp + xi * r, r, xr[u]);
+            if constexpr (K > 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + sg.poff + xi * r, r, ap[k][u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) keep(x[u][v]);
+            if constexpr (K != 0) {
+                // error feedback of the earlier iterations (reference :195-202), element by
+                // element; rows past the segment and inactive columns must stay 0 afterwards
+                const int32_t ru = row + u * stride;
+                const int32_t xi = ru < re ? ru : rb;
+                const bool valid = active && ru < re;
+                for (int k = 0; k < nres; ++k) {
+                    float pk[R];
+                    if constexpr (K > 0) {
+#pragma unroll
+                        for (int c = 0; c < R; ++c) pk[c] = ap[k < KC ? k : 0][u][c];
+                    } else {
+                        ld_factor<R>(gconst<float>(a.res.p[k]) + sg.poff + xi * r, r, pk);
+                    }
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        float qk[R];
+                        if constexpr (K > 0) {
+#pragma unroll
+                            for (int c = 0; c < R; ++c) qk[c] = bq[k < KC ? k : 0][v][c];
+                        } else {
+                            ld_factor<R>(gconst<float>(a.res.q[k]) + sg.qoff + (ccol + v) * r, r, qk);
+                        }
+                        x[u][v] = x[u][v] - dotr<R>(pk, qk);
+                    }
+                }
+#pragma unroll
+                for (int v = 0; v < V; ++v) x[u][v] = valid ? x[u][v] : 0.f;
+            }
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+                for (int c = 0; c < R; ++c) acc[v][c] = fmaf(x[u][v], xr[u][c], acc[v][c]);
+        }
+    }
+    even_epilogue<R, V>(a, sg, L, acc, red, ssl);
+}
+
+// Occupancy targets (waves per SIMD) per rank: the full-width path's registers, so that
+// every CU keeps enough 1 KB row loads in flight (PSGD_EVEN_WPE_R<rank> overrides for A/B runs)
+#ifndef PSGD_EVEN_WPE_R1
+#define PSGD_EVEN_WPE_R1 8
+#endif
+#ifndef PSGD_EVEN_WPE_R2
+#define PSGD_EVEN_WPE_R2 6
+#endif
+#ifndef PSGD_EVEN_WPE_R4
+#define PSGD_EVEN_WPE_R4 5
+#endif
+template <int R, int K>
+struct EvenWpe {
+    static constexpr int value = K != 0 ? 1 : R == 1 ? PSGD_EVEN_WPE_R1 : R == 2 ? PSGD_EVEN_WPE_R2 : R == 4 ? PSGD_EVEN_WPE_R4 : 1;
+};
+
+template <typename T, int R, int K>
+__global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe<R, K>::value))) void k_even(ProductArgs a) {
+    // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees vec == 0)
+    __shared__ __attribute__((aligned(16))) float red[kEvenNW * 64 * (R <= 8 ? 4 : 1) * R];
+    __shared__ float ssl[kEvenNW];
+    const int s0 = a.wg_seg[blockIdx.x], s1 = a.wg_seg[blockIdx.x + 1];
+    if (s0 >= s1) return;
+    // the next segment's descriptor and gradient pointer are loaded while this one streams
+    Seg nx = a.segs[s0];
+    const void* ng = a.grads[nx.tensor];
+    for (int si = s0; si < s1; ++si) {
+        const Seg sg = uni(nx);
+        const void* gp = uni(ng);
+        if (si + 1 < s1) {
+            nx = a.segs[si + 1];
+            ng = a.grads[nx.tensor];
+        }
+        if constexpr (R <= 8) {
+            if (sg.vec == 2) {
+                even_seg_full<T, R, K>(a, sg, gp, red, ssl);
+                continue;
+            }
+            if (sg.vec) {
+                even_seg<T, R, K, 4>(a, sg, gp, red, ssl);
+                continue;
+            }
+        }
+        even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+    }
+}
+
+template <typename T, int R>
+hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg, hipStream_t s) {
+    // register-cached error-feedback terms: up to 3 at ranks <= 4, 1 at rank 8 (more spill at
+    // the 256-VGPR cap of a 512-thread workgroup)
+    constexpr bool kCache = R <= 8;
+    const int K = (kCache && nres <= (R <= 4 ? 3 : 1)) ? nres : -1;
+    const dim3 grid(nwg), block(kEvenNT);
+    if constexpr (kCache) {
+        switch (K) {
+            case 0: k_even<T, R, 0><<<grid, block, 0, s>>>(a); break;
+            case 1: k_even<T, R, 1><<<grid, block, 0, s>>>(a); break;
+            case 2:
+                if constexpr (R <= 4) k_even<T, R, 2><<<grid, block, 0, s>>>(a);
+                break;
+            case 3:
+                if constexpr (R <= 4) k_even<T, R, 3><<<grid, block, 0, s>>>(a);
+                break;
+            default: k_even<T, R, -1><<<grid, block, 0, s>>>(a); break;
+        }
+    } else {
+        k_even<T, R, -1><<<grid, block, 0, s>>>(a);
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch_even(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s) {
+    if (nwg <= 0) return hipSuccess;
+    switch (R) {
+        case 1: return dispatch_even_r<T, 1>(nres, a, nwg, s);
+        case 2: return dispatch_even_r<T, 2>(nres, a, nwg, s);
+        case 4: return dispatch_even_r<T, 4>(nres, a, nwg, s);
+        case 8: return dispatch_even_r<T, 8>(nres, a, nwg, s);
+        case 16: return dispatch_even_r<T, 16>(nres, a, nwg, s);
+        case 32: return dispatch_even_r<T, 32>(nres, a, nwg, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace psgd

@@ -19,8 +19,6 @@
 // collective, :204-219): writes the output, reads no gradient.
 #pragma once
 
-#include <atomic>
-
 #include "psgd_stream.cuh"
 
 namespace psgd {
@@ -105,16 +103,6 @@ __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c
     }
 }
 
-// PL (panels in LDS): the factor panels X and Q_0 of the whole matrix live in LDS (`pan`,
-// [m][R] each, R floats per column) instead of per-thread registers, so a rank-4 row needs no
-// register panels and a 1024-thread workgroup keeps 16 waves of rows in flight.
-// Cross-wave row sums (row groups wider than a wave): 0 = dependent LDS reads in wave order,
-// 1 = a component's wave partials loaded together, 2 = wave-minor layout with 16-byte reads.
-// Build-time knob for A/B runs.
-#ifndef PSGD_FIN_XSUM
-#define PSGD_FIN_XSUM 0
-#endif
-
 // P_0 rows of a row block staged in LDS by the projection form: kFinRowsMax (psgd_internal.h)
 constexpr int kProjRows = kFinRowsMax;
 
@@ -124,9 +112,9 @@ constexpr int kProjRows = kFinRowsMax;
 // G - G X X^T (reference powersgd.py:185-230 with I = 2): the row pass needs X alone, no error
 // feedback term per element. The P state the reference keeps is P_1 = G X - P_0 R'^T (X^T X
 // = I), formed per row from the row sum.
-template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PL, bool PJ = false>
+template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PJ = false>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
-                                               float* red, float* pan, float* rqs = nullptr) {
+                                               float* red, float* rqs = nullptr) {
     constexpr int KC = K > 0 ? K : 1;
     constexpr int NW = NT / 64;
     const int r = d.r;
@@ -213,43 +201,9 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     }
     // factor row of column c (clamped to column 0 past the end of a ragged row)
     auto fcol = [&](int s, int v) { return ccol[s] + v < m ? ccol[s] + v : 0; };
-    float xq[PL ? 1 : SMAX][4][R];
-    float bq[PL ? 1 : KC][PL ? 1 : SMAX][4][R];
-    // LDS panels: component-major [R][mp] (mp = m rounded up to 4, zero padded) so that a
-    // lane's 4 consecutive columns of one component are ONE conflict-free ds_read_b128
-    const int64_t mp = (d.m + 3) & ~int64_t(3);
-    if constexpr (PL) {
-        // one column (R floats, one vector load when r == R) per thread and pass, 8 passes'
-        // loads in flight at once: the fill is a latency chain otherwise
-        constexpr int kFU = 8;
-        for (int64_t j0 = tid; j0 < mp; j0 += int64_t(kFU) * NT) {
-            float xv[kFU][R], bv[kFU][KC][R];
-#pragma unroll
-            for (int q = 0; q < kFU; ++q) {
-                const int64_t j = j0 + int64_t(q) * NT;
-                const int64_t jc = j < d.m ? j : 0;
-                ld_factor<R>(X + jc * r, r, xv[q]);
-#pragma unroll
-                for (int k = 0; k < KC; ++k)
-                    if (k < K) ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + jc * r, r, bv[q][k]);
-            }
-#pragma unroll
-            for (int q = 0; q < kFU; ++q) {
-                const int64_t j = j0 + int64_t(q) * NT;
-                if (j < mp) {
-#pragma unroll
-                    for (int c = 0; c < R; ++c) {
-                        const float x = j < d.m ? xv[q][c] : 0.f;
-                        pan[c * mp + j] = norm ? x / dn : x;  // matrix.div_ (:6)
-#pragma unroll
-                        for (int k = 0; k < KC; ++k)
-                            if (k < K) pan[(k + 1) * R * mp + c * mp + j] = j < d.m ? bv[q][k][c] : 0.f;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    } else {
+    float xq[SMAX][4][R];
+    float bq[KC][SMAX][4][R];
+    {
         // every panel load issued unconditionally (clamped columns) before any is consumed:
         // a load under a lane condition becomes a branch with its own wait, i.e. a chain of
         // SMAX * 4 * (K + 1) round trips before the first gradient row
@@ -285,47 +239,23 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                     if constexpr (R == 1) keep(xq[s][v][c]);
                 }
     }
-    // factor values of the 4 columns of segment s: registers, or R LDS vector reads
-    // (zero past the row end)
+    // factor values of the 4 columns of segment s (registers)
     auto segx = [&](int s, float (&o)[4][R]) {
-        if constexpr (PL) {
 #pragma unroll
-            for (int c = 0; c < R; ++c) {
-                const v4f q = *reinterpret_cast<const v4f*>(pan + c * mp + ccol[s]);
-                o[0][c] = act[s] ? q.x : 0.f;
-                o[1][c] = act[s] ? q.y : 0.f;
-                o[2][c] = act[s] ? q.z : 0.f;
-                o[3][c] = act[s] ? q.w : 0.f;
-            }
-        } else {
+        for (int v = 0; v < 4; ++v)
 #pragma unroll
-            for (int v = 0; v < 4; ++v)
-#pragma unroll
-                for (int c = 0; c < R; ++c) o[v][c] = xq[s][v][c];
-        }
+            for (int c = 0; c < R; ++c) o[v][c] = xq[s][v][c];
     };
     auto segb = [&](int k, int s, float (&o)[4][R]) {
-        if constexpr (PL) {
 #pragma unroll
-            for (int c = 0; c < R; ++c) {
-                const v4f q = *reinterpret_cast<const v4f*>(pan + (int64_t(k) + 1) * R * mp + c * mp + ccol[s]);
-                o[0][c] = q.x;
-                o[1][c] = q.y;
-                o[2][c] = q.z;
-                o[3][c] = q.w;
-            }
-        } else {
+        for (int v = 0; v < 4; ++v)
 #pragma unroll
-            for (int v = 0; v < 4; ++v)
-#pragma unroll
-                for (int c = 0; c < R; ++c) o[v][c] = bq[k < KC ? k : 0][s][v][c];
-        }
+            for (int c = 0; c < R; ++c) o[v][c] = bq[k < KC ? k : 0][s][v][c];
     };
 
     // segments past S load zeros (kOob) and drop their stores; their arithmetic is skipped
     // by a uniform branch
     auto seg_on = [&](int s) { return s < S; };
-    float ssq = 0.f;  // product-only: sum of squares of this thread's P rows (row-group leaders)
     auto process = [&](Batch& bt, int b) {
         const int64_t ib = row0 + (int64_t(b) * RGS + rg) * RB;
         int64_t ic[RB];
@@ -384,46 +314,6 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
                 for (int c = 0; c < R; ++c) dot[u][c] = sum_within(dot[u][c], Tg);
         } else {
-#if PSGD_FIN_XSUM == 2
-            // partials wave-minor ([u][c][wave]): a component's NW wave partials are NW / 4
-            // consecutive 16-byte LDS reads, all in flight at once, then added in wave order
-            float* buf = red + (b & 1) * NW * RB * R;
-#pragma unroll
-            for (int u = 0; u < RB; ++u)
-#pragma unroll
-                for (int c = 0; c < R; ++c) {
-                    dot[u][c] = wave_allsum(dot[u][c]);
-                    if (lane == 0) buf[(u * R + c) * NW + wave] = dot[u][c];
-                }
-            __syncthreads();
-            const int w0 = rg * (Tg >> 6), nw = Tg >> 6;
-#pragma unroll
-            for (int u = 0; u < RB; ++u)
-#pragma unroll
-                for (int c = 0; c < R; ++c) {
-                    const float* src = buf + (u * R + c) * NW;
-                    float pw[NW];
-                    if constexpr (NW % 4 == 0) {
-#pragma unroll
-                        for (int w = 0; w < NW; w += 4) {
-                            const v4f q = *reinterpret_cast<const v4f*>(src + w);
-                            pw[w] = q.x;
-                            pw[w + 1] = q.y;
-                            pw[w + 2] = q.z;
-                            pw[w + 3] = q.w;
-                        }
-                    } else {
-#pragma unroll
-                        for (int w = 0; w < NW; ++w) pw[w] = src[w];
-                    }
-                    // row group rg owns waves [w0, w0 + nw): nw is a power of two dividing NW
-                    float sum = 0.f;
-#pragma unroll
-                    for (int w = 0; w < NW; ++w)
-                        if (w >= w0 && w < w0 + nw) sum = (w == w0) ? pw[w] : sum + pw[w];
-                    dot[u][c] = sum;
-                }
-#else
             float* buf = red + (b & 1) * NW * RB * R;
 #pragma unroll
             for (int u = 0; u < RB; ++u)
@@ -438,23 +328,10 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
             for (int u = 0; u < RB; ++u)
 #pragma unroll
                 for (int c = 0; c < R; ++c) {
-#if PSGD_FIN_XSUM == 1
-                    // a component's wave partials read at once (one LDS round trip), added in
-                    // wave order
-                    float pw[NW];
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) pw[w] = buf[(w0 + (w < nw ? w : 0)) * RB * R + u * R + c];
-                    float sum = pw[0];
-#pragma unroll
-                    for (int w = 1; w < NW; ++w)
-                        if (w < nw) sum += pw[w];
-#else
                     float sum = buf[w0 * RB * R + u * R + c];
                     for (int w = 1; w < nw; ++w) sum += buf[(w0 + w) * RB * R + u * R + c];
-#endif
                     dot[u][c] = sum;
                 }
-#endif
         }
         // the local out-factor rows (history + the reference-visible P state, :189-193)
         if (tt == 0) {
@@ -480,11 +357,9 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             }
                             a.yloc[e] = y;
                             a.state[e] = y;
-                            if constexpr (!PJ) ssq = fmaf(y, y, ssq);  // PJ: never product-only
                         }
                 }
         }
-        if (!PJ && a.product_only) return;  // a later iteration forms residual and output
         // residual (and output at world size 1) from the registers
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -544,24 +419,13 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         load(ga, b + 2);
         if (b + 1 < nb) process(gb, b + 1);
     }
-    if (!PJ && a.product_only && a.ss_out) {
-        // this row block's sum of squares of P: row-group leaders in row-group order (fixed)
-        __syncthreads();  // the last batch's row sums may still be read from `red`
-        if (tt == 0) red[rg] = ssq;
-        __syncthreads();
-        if (tid == 0) {
-            float tot = 0.f;
-            for (int g2 = 0; g2 < RGS; ++g2) tot += red[g2];
-            a.ss_out[blockIdx.x - a.flat.nitems] = tot;
-        }
-    }
 }
 
 template <typename T, int R, int K, int SMAX, bool PJ = false>
 __device__ __forceinline__ void final_odd_block(const FinalArgs& a) {
     constexpr int NT = FinNT<R>::value, RB = FinRB<R>::value;
-    // batch row sums (2 buffers) and, in product-only mode, one sum of squares per row group
-    constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
+    // batch row sums (2 buffers)
+    constexpr int kRed = 2 * (NT / 64) * RB * R;
     __shared__ float red[kRed];
     __shared__ float rqs[PJ ? R * R + kProjRows * R : 1];
     // blocks [0, nitems): uncompressed tensors (first: beside the first wave of row blocks,
@@ -574,9 +438,9 @@ __device__ __forceinline__ void final_odd_block(const FinalArgs& a) {
     const Tile t = a.tiles[blockIdx.x - nf];
     const MatDesc d = a.mats[t.mat];
     if (d.vec)
-        final_odd_tile<T, R, K, SMAX, true, NT, RB, false, PJ>(a, d, t, red, nullptr, rqs);
+        final_odd_tile<T, R, K, SMAX, true, NT, RB, PJ>(a, d, t, red, rqs);
     else
-        final_odd_tile<T, R, K, SMAX, false, NT, RB, false, PJ>(a, d, t, red, nullptr, rqs);
+        final_odd_tile<T, R, K, SMAX, false, NT, RB, PJ>(a, d, t, red, rqs);
 }
 
 template <typename T, int R, int K, int SMAX>
@@ -587,31 +451,9 @@ __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
 // Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
 // CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
 template <typename T, int R, int SMAX>
-__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 && SMAX < 5 ? 4 : 1))) void k_final_proj(
+__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : 1))) void k_final_proj(
     FinalArgs a) {
     final_odd_block<T, R, 0, SMAX, true>(a);
-}
-
-// LDS-panel variant: 1024 threads (16 waves), one workgroup per CU (the panels take up to
-// ~150 KB), row groups of up to 512 threads (two rows per barrier at m = 4608).
-constexpr int kFinLdsNT = 1024;
-template <typename T, int R, int K, int SMAX>
-__global__ __launch_bounds__(kFinLdsNT) void k_final_lds(FinalArgs a) {
-    constexpr int NT = kFinLdsNT, RB = 1;
-    constexpr int kRed = 2 * (NT / 64) * RB * R > NT / 4 ? 2 * (NT / 64) * RB * R : NT / 4;
-    __shared__ float red[kRed];
-    extern __shared__ __attribute__((aligned(16))) float pan[];
-    const int nf = a.flat.nitems;
-    if (int(blockIdx.x) < nf) {
-        flat_pack_item<T, NT>(a.flat, blockIdx.x);
-        return;
-    }
-    const Tile t = a.tiles[blockIdx.x - nf];
-    const MatDesc d = a.mats[t.mat];
-    if (d.vec)
-        final_odd_tile<T, R, K, SMAX, true, NT, RB, true>(a, d, t, red, pan);
-    else
-        final_odd_tile<T, R, K, SMAX, false, NT, RB, true>(a, d, t, red, pan);
 }
 
 // output = sum_k alpha * (A_k B_k^T) on the lane-column tiles (same order as k_apply's
@@ -727,9 +569,6 @@ template <typename T, int R>
 hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s, waves);
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
-    if constexpr (R == 4) {  // projection form only: 5 segments at 2 waves per SIMD (PSGD_PROJ_S5)
-        if (smax <= 5 && nres == kFinProj) return launch_final_k<T, 4, 5, 0, true>(a, ntiles, s, waves);
-    }
     if constexpr (R <= 2) {
         if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
         if (smax <= 12 && nres <= 1) {
@@ -737,53 +576,6 @@ hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, 
                              : launch_final_k<T, R, 12, 1>(a, ntiles, s, waves);
         }
     }
-    return hipErrorInvalidValue;
-}
-
-template <typename T, int R, int SMAX, int K>
-hipError_t launch_final_lds_k(const FinalArgs& a, int ntiles, int lds_bytes, hipStream_t s, int* waves) {
-    const void* fn = reinterpret_cast<const void*>(&k_final_lds<T, R, K, SMAX>);
-    // opt in to > 64 KB of dynamic LDS once per instance AND device (the attribute is per
-    // device: a multi-device HostPowerSGD launches the same instance on several GPUs)
-    static std::atomic<uint64_t> attr_devs{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    const uint64_t bit = uint64_t(1) << (dev & 63);
-    if (!(attr_devs.load() & bit)) {
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 2048);
-        if (e != hipSuccess) return e;
-        attr_devs.fetch_or(bit);
-    }
-    if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
-        int blocks = 0;
-        hipFuncAttributes fa{};
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kFinLdsNT, size_t(lds_bytes));
-        if (e == hipSuccess) e = hipFuncGetAttributes(&fa, fn);
-        if (e != hipSuccess) return e;
-        *waves = fa.localSizeBytes > 0 ? 0 : blocks * (kFinLdsNT / 64) / 4;
-    }
-    if (ntiles == 0) return hipSuccess;
-    k_final_lds<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(kFinLdsNT), size_t(lds_bytes), s>>>(a);
-    return hipGetLastError();
-}
-
-// LDS-panel instances: ranks 2 and 4, at most one earlier term, rows of <= 3 segments of
-// 4 x 512 columns (row groups of up to 512 threads).
-template <typename T>
-hipError_t dispatch_final_lds(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
-                              hipStream_t s, int* waves) {
-#define PSGD_FL(RR, SS)                                                                               \
-    return nres == 0 ? launch_final_lds_k<T, RR, SS, 0>(a, ntiles, lds_bytes, s, waves)               \
-                     : launch_final_lds_k<T, RR, SS, 1>(a, ntiles, lds_bytes, s, waves)
-    if (nres > 1) return hipErrorInvalidValue;
-    if (R == 2) {
-        if (smax <= 2) PSGD_FL(2, 2);
-        if (smax <= 3) PSGD_FL(2, 3);
-    } else if (R == 4) {
-        if (smax <= 2) PSGD_FL(4, 2);
-        if (smax <= 3) PSGD_FL(4, 3);
-    }
-#undef PSGD_FL
     return hipErrorInvalidValue;
 }
 

@@ -37,19 +37,6 @@ struct MatDesc {
     int32_t fin_S;
     int32_t fin_rows;
     int32_t fin_pad;
-    // even product with the reduction folded in: this matrix's column strips own the ticket /
-    // sum-of-squares slots [slot0, slot0 + nstrip)
-    int32_t slot0;
-    int32_t pad2;
-};
-
-// One shape group, for the folded even reduction (joint norm, in-factor normalisation).
-struct GroupDesc {
-    int64_t poff, qoff;  // factor offsets of the group's first matrix
-    int64_t n, m;
-    int32_t r, count;
-    int32_t strips;      // strip slots of the group (sum over its matrices)
-    int32_t slot0;       // first strip slot of the group
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
@@ -59,15 +46,40 @@ struct Tile {
                      // load goes out beside the MatDesc load instead of after it)
 };
 
-// Reduction item for the partial-sum pass: 256 consecutive factor elements of one matrix.
+// Even-product work unit of the persistent k_even (psgd_even.cuh): rows [row0, row1) of one
+// column strip (L lanes x V columns) of one matrix. Workgroup w walks segments
+// [wg_seg[w], wg_seg[w + 1]) in order; segment boundaries split the plan (or a bucket of it)
+// into equal gradient byte ranges, one per workgroup, so a strip is cut only where a
+// workgroup's range ends: its column partials are few (one per segment, not one per small tile).
+// The matrix fields the pass needs are copied in, so a segment start is one descriptor load
+// and one gradient-pointer load (no MatDesc round trip in between).
+struct Seg {
+    int64_t m;           // columns of the matrix
+    int64_t poff, qoff;  // its P / Q panel offsets (floats)
+    int64_t part;        // float offset of this segment's partials [strip columns][r] in the workspace
+    int32_t row0, row1, strip;
+    int32_t tensor;      // gradient-table index of the matrix
+    int32_t ss;          // rank-1 norm fold: sum-of-squares slot of a strip-0 segment, else -1
+    int32_t r, lanes;
+    int32_t vec;         // 0: scalar columns; 1: 4-column vectors; 2: full-width strip fast path
+                         // (64 lanes x 4 columns, r == the plan's rank bucket, < 2^31 bytes)
+};
+
+// Reduction item for the partial-sum pass: up to 64 * per consecutive factor elements of one
+// matrix that share their partial layout: partial k of element start + j lies at
+// pbase + k * pstride + j (even: one column strip's segments; odd: the matrix's strips).
 constexpr int kRedElems = 64;  // fp64 plans: factor elements per reduction item (one per lane)
 constexpr int kRedItem = 256;  // fp32/bf16 plans: at most this many factor elements per reduction item
 constexpr int kRedWide = 64;   // ... when an element has at most this many partials (else 64)
 
 struct RedItem {
     int32_t mat, start;
-    int32_t per;  // fp32/bf16 plans: elements per lane (4: 256-element item; 1: 64 elements,
-                  // for factors with many partials, where 4 per lane is one CU's bandwidth)
+    int32_t per;     // fp32/bf16 plans: elements per lane (4: 256-element item; 1: 64 elements,
+                     // for factors with many partials, where 4 per lane is one CU's bandwidth)
+    int32_t cnt;     // elements in the item (<= 64 * per)
+    int64_t pbase;   // partial 0 of element `start` (floats from the partial workspace)
+    int32_t pstride; // floats between consecutive partials of one element
+    int32_t np;      // partials per element
 };
 
 // Orthonormalisation unit: rank 1 -> one shape GROUP (joint norm over count*k values);
@@ -116,31 +128,12 @@ struct ProductArgs {
     Terms res;           // error-feedback terms applied on the fly
     int32_t nres;
     // rank-1 iteration 0 with the norm folded (even product on the RAW state P): strip-0
-    // tiles write sum_rows P^2 of their row chunk to ss0[ss0_base[mat] + chunk]
+    // segments write sum_rows P^2 of their rows to ss0[seg.ss]
     float* ss0;
-    const int32_t* ss0_base;
-    // Even products with the partial reduction FOLDED IN (no k_reduce launch): the last tile
-    // of each column strip to finish (agent-scope release + ticket) sums the strip's partials,
-    // divides by the in-factor's joint norm (norm 1: from ss_in over grng_in; norm 2: of raw_in
-    // over the group) and writes yloc/state (+ the strip's sum of squares to ss_out); the last
-    // strip of a group then writes the normalised in-factor (raw_in / norm) to xstate and hx.
-    int32_t fold;
-    int32_t norm;
-    int32_t* cnt;
-    int32_t* gcnt;
-    const GroupDesc* groups;
-    float* yloc;
-    float* state;
-    float* ss_out;
-    const float* ss_in;
-    const int32_t* grng_in;
-    const float* raw_in;
-    float* xstate;
-    float* hx;    // even products, wave tiles (no fold): each wave of a workgroup takes its own tile
-    // (blockIdx * waves + wave of `ntiles`) and writes its partials from registers: no LDS
-    // reduction and no workgroup barrier in the epilogue
-    int32_t wave_tiles;
-    int32_t ntiles;
+    // even product (k_even): segments and per-workgroup [begin, end) (wg_seg[blockIdx],
+    // wg_seg[blockIdx + 1])
+    const Seg* segs;
+    const int32_t* wg_seg;
 };
 
 struct ApplyArgs {
@@ -227,11 +220,6 @@ struct FinalArgs {
     float* hx;
     int32_t ntiles;       // row blocks; flat pack items come first (as ApplyArgs)
     FlatArgs flat;
-    // product only (an odd iteration that is NOT the last one, world size 1): P rows are
-    // written (yloc/state) but neither the residual nor the output; each row block writes the
-    // sum of squares of its P rows to ss_out[block] (the next iteration's rank-1 joint norm)
-    int32_t product_only;
-    float* ss_out;
     // projection form (nres = kFinProj, see psgd_final.cuh): P_0 rows and R' per matrix
     const float* proj_p0;  // P layout
     const float* proj_r;   // Q layout: R' (r x r, row-major) at each matrix's qoff

@@ -22,27 +22,19 @@
 #include "psgd_internal.h"
 
 namespace psgd {
-hipError_t launch_product_f32(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
-hipError_t launch_product_bf16(int R, bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_even_f32(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s);
+hipError_t launch_even_bf16(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s);
+hipError_t launch_product_odd_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_product_odd_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_apply_f32(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_apply_bf16(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_odd_mfma_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_odd_mfma_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
-
 hipError_t launch_final_odd_f32(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
                                int* waves);
 hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s,
                                 int* waves);
 hipError_t launch_lowrank_out_f32(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
-hipError_t launch_final_lds_f32(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
-                               hipStream_t s, int* waves);
-hipError_t launch_final_lds_bf16(int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
-                                hipStream_t s, int* waves);
-hipError_t launch_final_lds(int dtype, int R, int nres, int smax, int lds_bytes, const FinalArgs& a, int ntiles,
-                            hipStream_t s, int* waves = nullptr) {
-    return dtype == PSGD_F32 ? launch_final_lds_f32(R, nres, smax, lds_bytes, a, ntiles, s, waves)
-                             : launch_final_lds_bf16(R, nres, smax, lds_bytes, a, ntiles, s, waves);
-}
 hipError_t launch_lowrank_out_bf16(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 
 hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
@@ -54,16 +46,16 @@ hipError_t launch_lowrank_out(int dtype, int R, int nterms, const ApplyArgs& a, 
     return dtype == PSGD_F32 ? launch_lowrank_out_f32(R, nterms, a, ntiles, s)
                              : launch_lowrank_out_bf16(R, nterms, a, ntiles, s);
 }
-
 hipError_t launch_odd_mfma(int dtype, int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     return dtype == PSGD_F32 ? launch_odd_mfma_f32(R, nres, a, ntiles, s)
                              : launch_odd_mfma_bf16(R, nres, a, ntiles, s);
 }
-
-hipError_t launch_product(int dtype, int R, bool even, int nres, const ProductArgs& a, int ntiles,
-                          hipStream_t s) {
-    return dtype == PSGD_F32 ? launch_product_f32(R, even, nres, a, ntiles, s)
-                             : launch_product_bf16(R, even, nres, a, ntiles, s);
+hipError_t launch_even(int dtype, int R, int nres, const ProductArgs& a, int nwg, hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_even_f32(R, nres, a, nwg, s) : launch_even_bf16(R, nres, a, nwg, s);
+}
+hipError_t launch_product_odd(int dtype, int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+    return dtype == PSGD_F32 ? launch_product_odd_f32(R, nres, a, ntiles, s)
+                             : launch_product_odd_bf16(R, nres, a, ntiles, s);
 }
 hipError_t launch_apply(int dtype, int R, int nterms, bool shared, const ApplyArgs& a, int ntiles,
                         hipStream_t s) {
@@ -163,20 +155,16 @@ struct FinGeom {
 #endif
 int fin_rb(int R) { return R == 4 ? 1 : PSGD_FIN_RB12; }   // == FinRB<R>
 int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
-// the two kernel forms: register panels (k_final_odd) and LDS panels (k_final_lds)
-struct FinForm {
-    int nt, tmax, rb;
-};
-FinForm fin_form(int R, bool lds) { return lds ? FinForm{1024, 512, 1} : FinForm{fin_nt(R), fin_nt(R), fin_rb(R)}; }
-// scap = 0: the widest row group (T = min(tmax, 4-column units rounded up to a power of
+// scap = 0: the widest row group (T = min(threads, 4-column units rounded up to a power of
 // two), fewest segments). scap > 0: the row group with the fewest idle lanes among
 // S <= scap (ties: the narrower group — more rows per batch and, at T <= 64, a row sum
 // within one wave instead of across waves through LDS); e.g. m = 576: T = 32, S = 5 (10 %
 // idle) rather than T = 256, S = 1 (44 % idle).
-FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int scap = 0) {
+FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems, int scap = 0) {
     FinGeom g;
+    const int nt = fin_nt(R), rb = fin_rb(R);
     const int64_t q4 = (m + 3) / 4;
-    g.T = int(std::min<int64_t>(f.tmax, pow2ceil(q4)));
+    g.T = int(std::min<int64_t>(nt, pow2ceil(q4)));
     g.S = int((q4 + g.T - 1) / g.T);
     if (scap > 0) {
         int64_t best = int64_t(g.S) * g.T;
@@ -190,13 +178,13 @@ FinGeom fin_geometry(int64_t n, int64_t m, FinForm f, int64_t fin_elems, int sca
             }
         }
     }
-    const int64_t batch = int64_t(f.nt / g.T) * f.rb;  // rows per workgroup batch
+    const int64_t batch = int64_t(nt / g.T) * rb;  // rows per workgroup batch
     int64_t rows = round_up(std::max<int64_t>(1, (fin_elems + m - 1) / m), batch);
     // a small matrix must still spread over several workgroups
     rows = std::min(rows, std::max(batch, round_up((n + 7) / 8, batch)));
     rows = std::min(rows, round_up(n, batch));
-    if (f.nt == f.tmax)  // register-panel form: at most kFinRowsMax rows (a multiple of batch)
-        rows = std::min(rows, std::max(batch, kFinRowsMax / batch * batch));
+    // at most kFinRowsMax rows (a multiple of batch)
+    rows = std::min(rows, std::max(batch, kFinRowsMax / batch * batch));
     g.rows = int(rows);
     g.ntiles = (n + rows - 1) / rows;
     return g;
@@ -311,6 +299,13 @@ struct DevScope {  // make `dev` current for the scope, restore afterwards
 
 }  // namespace
 
+// Persistent even product (k_even): workgroups per launch (CUs x workgroups per CU), at least
+// kEvenMinElems gradient elements per workgroup (small plans use fewer, fuller workgroups), at
+// most kMaxBuckets buckets (each bucket launch spreads over the whole chip).
+constexpr int kCUs = 256;                // MI355X
+constexpr int kEvenWgMax = 4 * kCUs;     // workgroups per launch (capacity)
+constexpr int kMaxBuckets = 8;
+
 struct psgd_plan {
     int rank = 0, iters = 0, dtype = 0;
     std::vector<std::vector<int64_t>> shapes;
@@ -328,55 +323,50 @@ struct psgd_plan {
     int64_t out_total = 0, ptot = 0, qtot = 0, fmax = 0;
     int rbucket = 1;
     int64_t tile_elems = 16384;
-    std::vector<Tile> tiles;     // lane-column tiles of every matrix (even products, apply)
+    std::vector<Tile> tiles;     // lane-column tiles of every matrix (apply, low-rank output)
     std::vector<Tile> tiles_ov;  // lane-column tiles of the odd-VALU matrices
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
     std::vector<Tile> tiles_fin; // row blocks of the fused final odd pass
-    bool fin_ok = false;         // every matrix fits the fused final odd pass
-    // per group [begin, end) of its row blocks in tiles_fin (for the product-only form's
-    // per-block sums of squares); false when the blocks of a group are not contiguous
-    std::vector<int32_t> grng_fin;
-    bool fin_grng_ok = false;
-    size_t o_grng_fin = 0, o_ss_fin = 0;
-    // even products with the reduction folded in (ProductArgs::fold): strip slots per matrix
-    // (MatDesc::slot0), group descriptors, per-group [begin, end) of strip slots
-    bool fold = false;
-    bool orth_chol = true;  // PSGD_ORTH_CHOL, read at bind (Cholesky-QR vs Householder)
-    std::vector<GroupDesc> gdesc;
-    std::vector<int32_t> grng_strip;
-    int64_t slots_cap = 0;
-    size_t o_cnt = 0, o_gcnt = 0, o_ss_strip = 0, o_grng_strip = 0, o_gdesc = 0;
-    bool fin_lds = false;        // ... in its LDS-panel form (k_final_lds)
+    bool fin_ok = false;         // every matrix fits the fused final odd pass (K-term form)
     bool fin_proj = false;       // ... in its projection form (I = 2, psgd_aggregate only)
-    bool proj_s5 = false;        // the projection form with 5-segment row groups (rank 4, opt-in)
+    bool orth_chol = true;       // PSGD_ORTH_CHOL, read at set_vec (Cholesky-QR vs Householder)
     int fin_smax = 0;
-    int fin_lds_bytes = 0;
-    int64_t fin_elems = 32768, fin_elems_lds = 65536, tiles_fin_cap = 0;
+    int64_t fin_elems = 32768, tiles_fin_cap = 0;
     int64_t tiles_cap = 0, tiles_om_cap = 0;
+    // even product (k_even): segments, per-workgroup segment ranges (wg_seg[w] .. wg_seg[w+1]),
+    // workgroups per CU and the minimum elements per workgroup (read at create)
+    std::vector<Seg> segs;
+    std::vector<int32_t> wg_seg;
+    int even_wpc = 4;
+    int64_t even_min = 16384;
+    int even_order = 0;  // 0: each workgroup walks down strips; 1: row blocks across strips
+    int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
+    // reduction items (rebuilt with the geometry): even items follow the segmentation
     std::vector<RedItem> red_even, red_odd;
     std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
+    int64_t red_even_cap = 0, red_odd_cap = 0;
     std::vector<OrthUnit> units_p, units_q;
     std::vector<OrthUnit> munits_p, munits_q;  // one unit per MATRIX (paper-code Gram-Schmidt)
     size_t o_munits_p = 0, o_munits_q = 0, o_rdst = 0, o_odst = 0;
     TableCache grad_tab, rdst_tab, odst_tab;  // device pointer tables (gradients, destinations)
     int64_t panel_p = 0, panel_q = 0;
-    int64_t part_floats = 0;
+    int64_t part_odd_floats = 0;  // odd partials [odd strips][n][r] per matrix; even ones follow
     double unc_floats = 0, comp_floats = 0;
     size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_tiles_fin = 0, o_red_even = 0,
            o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, o_grng_even = 0,
-           o_grng_odd = 0, o_ss = 0, ss_stride = 0, o_ss0 = 0, o_ss0_base = 0, o_grng_ss0 = 0,
+           o_grng_odd = 0, o_ss = 0, ss_stride = 0, o_ss0 = 0, o_grng_ss0 = 0, o_segs = 0, o_wg_seg = 0,
            ws_bytes = 0;
-    // rank-1 iteration-0 norm fold: per-(matrix, row chunk) sum-of-squares slots of the
-    // even product, and per group the [begin, end) slot range
-    std::vector<int32_t> ss0_base, grng_ss0;
-    int64_t ss0_slots = 0;
+    // rank-1 iteration-0 norm fold: per strip-0 segment a sum-of-squares slot, and per group the
+    // [begin, end) slot range
+    std::vector<int32_t> grng_ss0;
     // Buckets of whole shape groups (W > 1 overlap, psgd_plan_set_buckets): per bucket the
     // [begin, end) range of every launch list (all are in matrix order) and of the P/Q buffers.
     struct Span {
-        int32_t tiles[2], ov[2], om[2], fin[2], re[2], ro[2], up[2], uq[2];
+        int32_t tiles[2], ov[2], om[2], fin[2], re[2], ro[2], up[2], uq[2], wg[2];
         int64_t p[2], q[2];
     };
     std::vector<int32_t> bucket_gend;              // exclusive group end per bucket
+    std::vector<int32_t> bucket_wg;                // per bucket [begin, end) of its k_even workgroups
     std::vector<Span> spans;
     std::vector<int32_t> unit_group_p, unit_group_q;
     Span full_span() const {
@@ -389,6 +379,7 @@ struct psgd_plan {
         sp.ro[1] = int32_t(red_odd.size());
         sp.up[1] = int32_t(units_p.size());
         sp.uq[1] = int32_t(units_q.size());
+        sp.wg[1] = int32_t(wg_seg.empty() ? 0 : wg_seg.size() - 1);
         sp.p[1] = ptot;
         sp.q[1] = qtot;
         return sp;
@@ -420,6 +411,8 @@ struct psgd_plan {
             range(red_odd, rk, sp.ro);
             range(unit_group_p, [&](int32_t g) { return g >= g0 && g < g1; }, sp.up);
             range(unit_group_q, [&](int32_t g) { return g >= g0 && g < g1; }, sp.uq);
+            sp.wg[0] = bucket_wg[2 * b];
+            sp.wg[1] = bucket_wg[2 * b + 1];
             sp.p[0] = groups[g0].poff;
             sp.q[0] = groups[g0].qoff;
             sp.p[1] = g1 < int32_t(groups.size()) ? groups[g1].poff : ptot;
@@ -441,7 +434,7 @@ struct psgd_plan {
     float* Q = nullptr;
     char* ws = nullptr;
     void* out_now = nullptr;  // psgd_aggregate's output buffer (fused final pass)
-    // benchmark timing of k_apply: event pairs recorded on the launch stream
+    // benchmark timing of the final pass: event pairs recorded on the launch stream
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
@@ -459,30 +452,8 @@ struct psgd_plan {
     size_t o_gram = 0, o_uitems = 0;
     std::vector<int32_t> uitems, red_even_b, red_even_e;
     bool qfold(int64_t step, bool agg) const { return qfold_ok && iters == 2 && proj_final(step, agg); }
-    // World-size-1 steps as HIP graphs (psgd_plan_set_graphs): one captured graph per distinct
-    // (pointer-table slots, output pointers, parity class), replayed with one launch; the buckets
-    // (when set and overlap is on) run on two side streams forked inside the graph.
-    struct GraphEntry {
-        uint64_t key[6];
-        hipGraphExec_t exec;
-        uint64_t stamp;
-    };
-    bool use_graphs = false, overlap = false;  // both opt-in: slower on ROCm 7.2
-    std::vector<GraphEntry> graphs;
-    uint64_t graph_clock = 0;
-    hipStream_t gstream = nullptr, side[2] = {nullptr, nullptr};
-    hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-    void drop_graphs() {
-        for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
-        graphs.clear();
-    }
 
     ~psgd_plan() {
-        drop_graphs();
-        for (hipStream_t st : {gstream, side[0], side[1]})
-            if (st) (void)hipStreamDestroy(st);
-        for (hipEvent_t e : {ev_in, ev_out, ev_fork, ev_join[0], ev_join[1]})
-            if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_pool) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -506,6 +477,8 @@ struct psgd_plan {
         f64_part_off.clear();
         f64_part = 0;
         vec_now = base_vec;
+        red_even.clear();
+        red_odd.clear();
         for (size_t i = 0; i < mats.size(); ++i) {
             MatDesc& d = mats[i];
             d.vec = 0;
@@ -518,28 +491,227 @@ struct psgd_plan {
             for (int64_t b = 0; b * d.chunk_rows < d.n; ++b) f64_apply.push_back(Tile{int32_t(i), 0, int32_t(b), 0});
             f64_part_off.push_back(f64_part);
             f64_part += int64_t(d.nchunk) * kWaves * d.m * d.r;
+            // k_f64_reduce: 64 consecutive Q elements per item (start only)
+            for (int64_t s = 0; s < d.m * d.r; s += kRedElems)
+                red_even.push_back(RedItem{int32_t(i), int32_t(s), 1, int32_t(std::min<int64_t>(kRedElems, d.m * d.r - s)), 0, 0, 0});
         }
     }
     template <typename T>
     T* dev(size_t off) const { return reinterpret_cast<T*>(ws + off); }
     bool even(int64_t step, int it) const { return ((step * iters + it) % 2) == 0; }
 
+    // Even-product segmentation (k_even) and every reduction item list, for the current strip
+    // geometry and buckets. Per bucket (or the whole plan), the gradient elements of its
+    // matrices (walked matrix -> strip -> row) are cut into nwg equal ranges, one per workgroup;
+    // a segment ends at a strip end or at a workgroup's range end. Partials: per strip, its
+    // segments' [W x r] slabs in row order (W = lanes x V strip columns).
+    void build_reduction() {
+        segs.clear();
+        wg_seg.clear();
+        bucket_wg.clear();
+        red_even.clear();
+        red_odd.clear();
+        red_even_b.assign(mats.size(), 0);
+        red_even_e.assign(mats.size(), 0);
+        grng_even.assign(2 * groups.size(), 0);
+        grng_odd.assign(2 * groups.size(), 0);
+        grng_ss0.assign(2 * groups.size(), 0);
+        std::vector<int32_t> ends = bucket_gend;
+        if (ends.empty()) ends.push_back(int32_t(groups.size()));
+        // pass 1: segments per bucket
+        std::vector<std::vector<int32_t>> nseg(mats.size());  // per matrix, per strip: segment count
+        for (size_t i = 0; i < mats.size(); ++i) nseg[i].assign(size_t(mats[i].nstrip), 0);
+        size_t mi = 0;
+        for (int32_t g1 : ends) {
+            size_t m0 = mi;
+            while (mi < mats.size() && mats[mi].group < g1) ++mi;
+            int64_t total = 0;
+            for (size_t i = m0; i < mi; ++i) total += mats[i].n * mats[i].m;
+            const int64_t nwg = std::max<int64_t>(
+                1, std::min<int64_t>(int64_t(even_wpc) * kCUs, (total + even_min - 1) / std::max<int64_t>(even_min, 1)));
+            bucket_wg.push_back(int32_t(wg_seg.size()));
+            int64_t cum = 0, w = 0;
+            wg_seg.push_back(int32_t(segs.size()));
+            auto bound = [&](int64_t ww) { return (ww + 1) * total / nwg; };
+            auto make = [&](size_t i, int s, int64_t r0, int64_t r1) {
+                const MatDesc& d = mats[i];
+                Seg sg{};
+                sg.m = d.m;
+                sg.poff = d.poff;
+                sg.qoff = d.qoff;
+                sg.row0 = int32_t(r0);
+                sg.row1 = int32_t(r1);
+                sg.strip = s;
+                sg.tensor = d.tensor;
+                sg.ss = -1;
+                sg.r = d.r;
+                sg.lanes = d.lanes;
+                sg.vec = d.vec;
+                // full-width strips of an r == R matrix take k_even's scalar-row fast path
+                if (d.vec && d.lanes == 64 && d.r == rbucket && rbucket <= 8) sg.vec = 2;
+                sg.part = int64_t(i);  // matrix index for now (pass 2)
+                segs.push_back(sg);
+                ++nseg[i][size_t(s)];
+            };
+            if (even_order == 1) {
+                // row blocks of ~total / nwg elements per strip, emitted block-major and strip-
+                // minor, each workgroup taking whole blocks: the workgroups that run side by side
+                // read the adjacent strips of the same rows (DRAM page locality), as a tile grid
+                const int64_t target = std::max<int64_t>(1, total / nwg);
+                for (size_t i = m0; i < mi; ++i) {
+                    const MatDesc& d = mats[i];
+                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                    const int64_t es = dtype == PSGD_BF16 ? 2 : 4;
+                    const int64_t seg_max = std::max<int64_t>(1, ((int64_t(1) << 30) / (d.m * es)) - 64);
+                    const int64_t h = std::min(seg_max, std::max<int64_t>(1, (target + W / 2) / W));
+                    for (int64_t r0 = 0; r0 < d.n; r0 += h) {
+                        const int64_t r1 = std::min(d.n, r0 + h);
+                        for (int s = 0; s < d.nstrip; ++s) {
+                            const int64_t cost = (r1 - r0) * std::min<int64_t>(W, d.m - s * W);
+                            if (w < nwg - 1 && segs.size() > size_t(wg_seg.back()) && 2 * cum + cost > 2 * bound(w)) {
+                                ++w;
+                                wg_seg.push_back(int32_t(segs.size()));
+                            }
+                            make(i, s, r0, r1);
+                            cum += cost;
+                        }
+                    }
+                }
+            } else {
+                for (size_t i = m0; i < mi; ++i) {
+                    const MatDesc& d = mats[i];
+                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                    for (int s = 0; s < d.nstrip; ++s) {
+                        const int64_t cols = std::min<int64_t>(W, d.m - s * W);
+                        // k_even addresses a segment with 32-bit offsets: at most 2^30 bytes each
+                        const int64_t es = dtype == PSGD_BF16 ? 2 : 4;
+                        const int64_t seg_max = std::max<int64_t>(1, ((int64_t(1) << 30) / (d.m * es)) - 64);
+                        int64_t r0 = 0;
+                        while (r0 < d.n) {
+                            int64_t take = std::min(d.n - r0, seg_max);
+                            if (w < nwg - 1) {
+                                const int64_t fit = (bound(w) - cum + cols / 2) / cols;  // rows to this range's end
+                                if (fit <= 0) {
+                                    ++w;
+                                    wg_seg.push_back(int32_t(segs.size()));
+                                    continue;
+                                }
+                                take = std::min(take, fit);
+                            }
+                            make(i, s, r0, r0 + take);
+                            cum += take * cols;
+                            r0 += take;
+                            if (w < nwg - 1 && cum * nwg >= (w + 1) * total) {  // this range is full
+                                ++w;
+                                wg_seg.push_back(int32_t(segs.size()));
+                            }
+                        }
+                    }
+                }
+            }
+            while (int64_t(wg_seg.size()) - bucket_wg.back() < nwg + 1) wg_seg.push_back(int32_t(segs.size()));
+            bucket_wg.push_back(int32_t(wg_seg.size()) - 1);
+        }
+        // wg_seg holds nwg + 1 bounds per bucket; the buckets' ranges are concatenated so that
+        // workgroup w of the whole launch reads wg_seg[w], wg_seg[w + 1]: drop each bucket's
+        // closing bound except the last
+        {
+            std::vector<int32_t> flat;
+            std::vector<int32_t> bw;
+            for (size_t b = 0; b * 2 < bucket_wg.size(); ++b) {
+                const int32_t lo = bucket_wg[2 * b], hi = bucket_wg[2 * b + 1];
+                bw.push_back(int32_t(flat.size()));
+                for (int32_t k = lo; k < hi; ++k) flat.push_back(wg_seg[size_t(k)]);
+                bw.push_back(int32_t(flat.size()));
+            }
+            flat.push_back(int32_t(segs.size()));
+            wg_seg.swap(flat);
+            bucket_wg.swap(bw);
+        }
+        // pass 2: partial slabs (per matrix, per strip, segments in row order) and ss slots
+        std::vector<std::vector<int64_t>> base(mats.size());
+        int64_t off = (part_odd_floats + 3) & ~int64_t(3);
+        for (size_t i = 0; i < mats.size(); ++i) {
+            const MatDesc& d = mats[i];
+            const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+            base[i].assign(size_t(d.nstrip), 0);
+            for (int s = 0; s < d.nstrip; ++s) {
+                base[i][size_t(s)] = off;
+                off += (int64_t(nseg[i][size_t(s)]) * W * d.r + 3) & ~int64_t(3);
+            }
+        }
+        std::vector<std::vector<int32_t>> kseg(mats.size());
+        for (size_t i = 0; i < mats.size(); ++i) kseg[i].assign(size_t(mats[i].nstrip), 0);
+        int32_t ss = 0;
+        // strip-0 segments get consecutive slots in matrix order (a group's slots contiguous)
+        std::vector<std::vector<int32_t>> s0(mats.size());
+        for (Seg& sg : segs) {
+            const size_t i = size_t(sg.part);
+            const MatDesc& d = mats[i];
+            const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+            const int32_t k = kseg[i][size_t(sg.strip)]++;
+            sg.part = base[i][size_t(sg.strip)] + int64_t(k) * W * d.r;
+            if (sg.strip == 0) s0[i].push_back(int32_t(&sg - segs.data()));
+        }
+        for (size_t i = 0; i < mats.size(); ++i) {
+            const int g = mats[i].group;
+            if (i == 0 || mats[i - 1].group != g) grng_ss0[2 * g] = ss;
+            for (int32_t si : s0[i]) segs[size_t(si)].ss = ss++;
+            grng_ss0[2 * g + 1] = ss;
+        }
+        // reduction items: even ones per strip (its segments' partials), odd ones per matrix
+        for (size_t i = 0; i < mats.size(); ++i) {
+            const MatDesc& d = mats[i];
+            const int g = d.group;
+            const bool first = i == 0 || mats[i - 1].group != g;
+            if (first) {
+                grng_even[2 * g] = int32_t(red_even.size());
+                grng_odd[2 * g] = int32_t(red_odd.size());
+            }
+            const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+            red_even_b[i] = int32_t(red_even.size());
+            for (int s = 0; s < d.nstrip; ++s) {
+                const int np = nseg[i][size_t(s)];
+                const int pe = np > kRedWide ? 1 : 4;
+                const int64_t e0 = s * W * d.r, e1 = std::min<int64_t>((s + 1) * W, d.m) * d.r;
+                for (int64_t e = e0; e < e1; e += 64 * pe)
+                    red_even.push_back(RedItem{int32_t(i), int32_t(e), pe, int32_t(std::min<int64_t>(64 * pe, e1 - e)),
+                                               base[i][size_t(s)] + (e - e0), int32_t(W * d.r), np});
+            }
+            red_even_e[i] = int32_t(red_even.size());
+            const int npo = d.odd_nstrip;
+            const int po = npo > kRedWide ? 1 : 4;
+            for (int64_t e = 0; e < d.n * d.r; e += 64 * po)
+                red_odd.push_back(RedItem{int32_t(i), int32_t(e), po, int32_t(std::min<int64_t>(64 * po, d.n * d.r - e)),
+                                          d.part_odd + e, int32_t(d.n * d.r), npo});
+            grng_even[2 * g + 1] = int32_t(red_even.size());
+            grng_odd[2 * g + 1] = int32_t(red_odd.size());
+        }
+        // folded orthonormalisation: per Q unit (one matrix each) its even item range
+        uitems.clear();
+        if (qfold_ok) {
+            for (const OrthUnit& u : units_q)
+                for (size_t i = 0; i < mats.size(); ++i)
+                    if (mats[i].qoff == u.off) {
+                        uitems.push_back(red_even_b[i]);
+                        uitems.push_back(red_even_e[i]);
+                    }
+        }
+    }
+
     void set_vec(const std::vector<int>& vec) {
-        drop_graphs();  // captured launch grids / tile lists may change
         vec_now = vec;
         tiles.clear();
         tiles_ov.clear();
         tiles_om.clear();
         tiles_fin.clear();
-        // PSGD_FUSE_FINAL: 0 off; 1 (default) register panels at ranks 1-2; 2 also allows
-        // the register form at rank 4 (it fits 512-thread rows, but one row per barrier is
-        // too little in flight: slower than unfused); 3 the LDS-panel form at ranks 2-4.
-        // Both rank-4 forms are correct (tests/test_gpu_final.py) but measure slower than
-        // the unfused kernels on ResNet-50 (k_final_lds 96-107 us vs 56 us for k_apply +
-        // 22 us odd product, profiles/r01/sweep_final_lds.txt), so they are opt-in.
+        // PSGD_FUSE_FINAL: 0 off; 1 (default) the K-term fused final at ranks 1-2; 2 also at
+        // rank 4 (it fits 512-thread rows but measured slower than the unfused kernels on
+        // ResNet-50, profiles/r01/sweep_final_lds.txt; correct, tests/test_gpu_final.py)
         const int64_t fuse_mode = env_int("PSGD_FUSE_FINAL", 1);
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
+        int64_t podd = 0;
         for (size_t i = 0; i < mats.size(); ++i) {
             MatDesc& d = mats[i];
             const Geom g = geometry(d.n, d.m, d.r, vec[i], tile_elems);
@@ -551,7 +723,7 @@ struct psgd_plan {
             const OddGeom og = odd_geometry(d.n, d.m, tile_elems);
             // the MFMA kernel addresses a tile through a buffer descriptor (< 2^31 bytes)
             const int64_t span = ((int64_t(og.chunk_rows) - 1) * d.m + og.sw) * (dtype == PSGD_BF16 ? 2 : 4);
-            // r <= 4: every odd tile stays in ONE k_product<odd> launch (row layout with a
+            // r <= 4: every odd tile stays in ONE k_product_odd launch (row layout with a
             // reduce-scatter on full-width strips, lane sums on narrow ones); the MFMA kernel
             // pays for itself only for wider factors (16 output columns per instruction)
             const bool valu = use_rows && d.r <= 4;
@@ -571,100 +743,43 @@ struct psgd_plan {
                 d.odd_sw = d.odd_chunk_rows = 0;
                 d.odd_nstrip = g.nstrip;
             }
+            // odd partials [odd strips][n][r], 16-byte aligned slabs (k_reduce's vector loads)
+            d.part_odd = podd = (podd + 3) & ~int64_t(3);
+            podd += int64_t(d.odd_nstrip) * d.n * d.r;
+            d.part_even = 0;
         }
-        // strip slots of the folded even reduction (matrix order; a group's slots contiguous)
-        gdesc.assign(groups.size(), GroupDesc{});
-        grng_strip.assign(2 * groups.size(), 0);
-        {
-            int32_t slot = 0;
-            for (size_t i = 0; i < mats.size(); ++i) {
-                MatDesc& d = mats[i];
-                GroupDesc& gd = gdesc[d.group];
-                if (i == 0 || mats[i - 1].group != d.group) {
-                    const auto& gr = groups[d.group];
-                    gd = GroupDesc{gr.poff, gr.qoff, gr.n, gr.m, gr.r, int32_t(gr.tensors.size()), 0, slot};
-                    grng_strip[2 * d.group] = slot;
-                }
-                d.slot0 = slot;
-                slot += d.nstrip;
-                gd.strips += d.nstrip;
-                grng_strip[2 * d.group + 1] = slot;
-            }
-        }
+        part_odd_floats = podd;
         fin_ok = false;
-        fin_lds = false;
         fin_proj = false;
         orth_chol = env_int("PSGD_ORTH_CHOL", 1) != 0;
         // buffer descriptors address one matrix: keep each below 2^31 bytes
         bool small = true;
-        int64_t mmax = 0;
-        for (const MatDesc& d : mats) {
-            small = small && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
-            mmax = std::max(mmax, d.m);
-        }
-        auto try_form = [&](bool lds) {
-            const FinForm f = fin_form(rbucket, lds);
-            int smax = 0;
-            for (const MatDesc& d : mats) smax = std::max(smax, fin_geometry(d.n, d.m, f, 0).S);
+        for (const MatDesc& d : mats) small = small && d.n * d.m * (dtype == PSGD_BF16 ? 2 : 4) < (int64_t(1) << 31);
+        int smax = 0;
+        for (const MatDesc& d : mats) smax = std::max(smax, fin_geometry(d.n, d.m, rbucket, 0).S);
+        // >= 2 waves per SIMD resident (the register arrays scale with S * 4 * r)
+        auto fits = [&](int nres) {
             int waves = 0;
             FinalArgs none{};
-            if (lds) {
-                const int64_t bytes = (1 + std::min(iters - 1, 1)) * ((mmax + 3) & ~int64_t(3)) * rbucket *
-                                      int64_t(sizeof(float));
-                if (iters - 1 > 1 || bytes > 150 * 1024) return false;
-                fin_lds_bytes = int(bytes);
-                // one 16-wave workgroup per CU = 4 waves per SIMD
-                return launch_final_lds(dtype, rbucket, iters - 1, smax, fin_lds_bytes, none, 0, nullptr,
-                                        &waves) == hipSuccess && waves >= 4;
-            }
-            // >= 2 waves per SIMD resident (the register arrays scale with S * 4 * r)
             return fin_bucket(smax) > 0 &&
-                   launch_final_odd(dtype, rbucket, iters - 1, fin_bucket(smax), none, 0, nullptr, &waves) ==
-                       hipSuccess &&
+                   launch_final_odd(dtype, rbucket, nres, fin_bucket(smax), none, 0, nullptr, &waves) == hipSuccess &&
                    waves >= 2;
         };
-        if (fuse_mode != 0 && small) {
-            if (fuse_mode != 3 && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2))) fin_ok = try_form(false);
-            if (!fin_ok && fuse_mode == 3 && (rbucket == 2 || rbucket == 4)) fin_ok = fin_lds = try_form(true);
-        }
+        if (fuse_mode != 0 && small && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2))) fin_ok = fits(iters - 1);
         // Projection form (psgd_final.cuh): two power iterations at world size 1, ranks 2 and 4,
         // the last iteration's in-factor orthonormalised by Cholesky-QR (which leaves R').
         // Same register-panel geometry as the K-term form, so both can share the tile list.
-        if (fuse_mode != 0 && small && !fin_lds && iters == 2 && (rbucket == 2 || rbucket == 4) && orth_chol &&
-            env_int("PSGD_FIN_PROJ", 1) != 0) {
-            const FinForm f = fin_form(rbucket, false);
-            int smax = 0;
-            for (const MatDesc& d : mats) smax = std::max(smax, fin_geometry(d.n, d.m, f, 0).S);
-            int waves = 0;
-            FinalArgs none{};
-            fin_proj = fin_bucket(smax) > 0 &&
-                       launch_final_odd(dtype, rbucket, kFinProj, fin_bucket(smax), none, 0, nullptr, &waves) ==
-                           hipSuccess &&
-                       waves >= 2;
-            // opt-in: rank 4 with up to 5 register segments (fewer idle lanes on 9c-column rows,
-            // 2 waves per SIMD); only when no K-term fused form shares the tile list
-            proj_s5 = false;
-            if (fin_proj && !fin_ok && rbucket == 4 && env_int("PSGD_PROJ_S5", 0) != 0) {
-                int w5 = 0;
-                proj_s5 = launch_final_odd(dtype, 4, kFinProj, 5, none, 0, nullptr, &w5) == hipSuccess && w5 >= 2;
-            }
-        }
+        if (fuse_mode != 0 && small && iters == 2 && (rbucket == 2 || rbucket == 4) && orth_chol &&
+            env_int("PSGD_FIN_PROJ", 1) != 0)
+            fin_proj = fits(kFinProj);
         fin_smax = 0;
         if (fin_ok || fin_proj) {
-            const FinForm f = fin_form(rbucket, fin_lds);
-            const int64_t elems = fin_lds ? fin_elems_lds : fin_elems;
             // segments per row up to the kernel bucket the widest groups already need
             // (at most 5: the exact-S bodies), for fewer idle lanes
-            int scap = 0;
-            if (env_int("PSGD_FIN_GEOM", 1) && !fin_lds) {
-                for (const MatDesc& d : mats) scap = std::max(scap, fin_geometry(d.n, d.m, f, 0).S);
-                scap = proj_s5 ? 5 : std::min(fin_bucket(scap), 5);
-                if (const int64_t sc = env_int("PSGD_FIN_SCAP", 0))  // A/B knob: segment cap
-                    scap = int(std::min<int64_t>(sc, fin_smax_inst(rbucket)));
-            }
+            const int scap = env_int("PSGD_FIN_GEOM", 1) ? std::min(fin_bucket(smax), 5) : 0;
             for (size_t i = 0; i < mats.size(); ++i) {
                 MatDesc& d = mats[i];
-                const FinGeom fg = fin_geometry(d.n, d.m, f, elems, scap);
+                const FinGeom fg = fin_geometry(d.n, d.m, rbucket, fin_elems, scap);
                 d.fin_T = fg.T;
                 d.fin_S = fg.S;
                 d.fin_rows = fg.rows;
@@ -672,40 +787,7 @@ struct psgd_plan {
                 for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), d.tensor});
             }
         }
-        // Optional: largest tiles first (a greedy longest-processing-time order for the
-        // dispatcher, which hands out workgroups in index order as slots free up).
-        // Measured neutral-to-worse on ResNet-50 (profiles/r01), so off by default.
-        if (env_int("PSGD_SORT_TILES", 0) && bucket_gend.empty()) {  // buckets need matrix order
-            auto cost_fin = [&](const Tile& t) {
-                const MatDesc& d = mats[t.mat];
-                return std::min<int64_t>(d.fin_rows, d.n - int64_t(t.chunk) * d.fin_rows) * d.m;
-            };
-            auto cost_col = [&](const Tile& t) {
-                const MatDesc& d = mats[t.mat];
-                const int64_t w = int64_t(d.lanes) * (d.vec ? 4 : 1);
-                return std::min<int64_t>(d.chunk_rows, d.n - int64_t(t.chunk) * d.chunk_rows) *
-                       std::min<int64_t>(w, d.m - int64_t(t.strip) * w);
-            };
-            auto by = [](auto cost) {
-                return [cost](const Tile& a, const Tile& b) { return cost(a) > cost(b); };
-            };
-            std::stable_sort(tiles_fin.begin(), tiles_fin.end(), by(cost_fin));
-            std::stable_sort(tiles.begin(), tiles.end(), by(cost_col));
-            std::stable_sort(tiles_ov.begin(), tiles_ov.end(), by(cost_col));
-        }
-        grng_fin.assign(2 * groups.size(), 0);
-        fin_grng_ok = fin_ok;
-        for (size_t g = 0; g < groups.size() && fin_grng_ok; ++g) {
-            int32_t b = -1, e = -1;
-            for (size_t i = 0; i < tiles_fin.size(); ++i)
-                if (mats[tiles_fin[i].mat].group == int32_t(g)) {
-                    if (b < 0) b = int32_t(i);
-                    else if (e != int32_t(i)) fin_grng_ok = false;  // not contiguous
-                    e = int32_t(i) + 1;
-                }
-            grng_fin[2 * g] = b < 0 ? 0 : b;
-            grng_fin[2 * g + 1] = e < 0 ? 0 : e;
-        }
+        build_reduction();
         if (!bucket_gend.empty()) build_spans();
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits); `agg`: the caller
@@ -713,12 +795,6 @@ struct psgd_plan {
     bool fused_final(int64_t step, bool agg) const { return (fin_ok || (agg && fin_proj)) && !even(step, iters - 1); }
     // the fused last iteration takes the projection form
     bool proj_final(int64_t step, bool agg) const { return agg && fin_proj && !even(step, iters - 1); }
-    // an odd iteration before the last one, at world size 1 (fuse): P in the row-resident final
-    // kernel in product-only form (no partials, no reduction launch)
-    bool fin_prod(int64_t step, int it, bool fuse) const {
-        return fuse && fin_ok && fin_grng_ok && it < iters - 1 && !even(step, it) &&
-               env_int("PSGD_FIN_PRODUCT", 0) != 0;  // opt-in: neutral-to-slower on cfg5
-    }
     bool fused_final_at(int64_t step, int it, bool agg) const { return it == iters - 1 && fused_final(step, agg); }
 
     int upload_tiles() const;
@@ -771,14 +847,25 @@ int refresh_pointers(psgd_plan* p, void* const* grads, hipStream_t stream) {
 }  // namespace
 
 int psgd_plan::upload_tiles() const {
+    // the lists follow the geometry and the buckets: never past the capacities carved at create
+    if (int64_t(segs.size()) > segs_cap || int64_t(wg_seg.size()) > int64_t(kMaxBuckets) * kEvenWgMax + 1 ||
+        int64_t(red_even.size()) > red_even_cap || int64_t(red_odd.size()) > red_odd_cap)
+        return fail(PSGD_ERR_STATE, "internal: work lists exceed their workspace capacity");
     if (int st = upload(dev<void>(o_mats), mats.data(), mats.size() * sizeof(MatDesc))) return st;
     if (int st = upload(dev<void>(o_tiles), tiles.data(), tiles.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_fin), tiles_fin.data(), tiles_fin.size() * sizeof(Tile))) return st;
-    if (int st = upload(dev<void>(o_grng_fin), grng_fin.data(), grng_fin.size() * sizeof(int32_t))) return st;
-    if (int st = upload(dev<void>(o_gdesc), gdesc.data(), gdesc.size() * sizeof(GroupDesc))) return st;
-    if (int st = upload(dev<void>(o_grng_strip), grng_strip.data(), grng_strip.size() * sizeof(int32_t))) return st;
-    return upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile));
+    if (int st = upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile))) return st;
+    if (int st = upload(dev<void>(o_segs), segs.data(), segs.size() * sizeof(Seg))) return st;
+    if (int st = upload(dev<void>(o_wg_seg), wg_seg.data(), wg_seg.size() * sizeof(int32_t))) return st;
+    if (int st = upload(dev<void>(o_red_even), red_even.data(), red_even.size() * sizeof(RedItem))) return st;
+    if (int st = upload(dev<void>(o_red_odd), red_odd.data(), red_odd.size() * sizeof(RedItem))) return st;
+    if (int st = upload(dev<void>(o_grng_even), grng_even.data(), grng_even.size() * sizeof(int32_t))) return st;
+    if (int st = upload(dev<void>(o_grng_odd), grng_odd.data(), grng_odd.size() * sizeof(int32_t))) return st;
+    if (int st = upload(dev<void>(o_grng_ss0), grng_ss0.data(), grng_ss0.size() * sizeof(int32_t))) return st;
+    if (qfold_ok)
+        if (int st = upload(dev<void>(o_uitems), uitems.data(), uitems.size() * sizeof(int32_t))) return st;
+    return PSGD_OK;
 }
 
 namespace {
@@ -900,9 +987,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
                                  ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
                                  : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
-        // LDS form: one workgroup per CU that first loads the matrix's panels, so larger
-        // blocks (~2 rounds over 256 CUs)
-        p->fin_elems_lds = std::max<int64_t>(4096, env_int("PSGD_FIN_ELEMS_LDS", std::max<int64_t>(16384, total / 512)));
+        // persistent even product: workgroups per CU, minimum gradient elements per workgroup
+        p->even_wpc = int(std::min<int64_t>(4, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
+        p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
+        p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
     }
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
@@ -955,74 +1043,58 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->qtot = qoff;
     p->fmax = std::max(poff, qoff);
 
-    // partial-sum slabs sized for either vector width; reduction items
-    for (size_t i = 0; i < p->mats.size(); ++i) {
-        MatDesc& md = p->mats[i];
-        const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
-        const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
-        const OddGeom og = odd_geometry(md.n, md.m, p->tile_elems);
-        // 16-byte aligned partial slabs (k_reduce's vector loads)
-        md.part_even = p->part_floats = (p->part_floats + 3) & ~int64_t(3);
-        p->part_floats += std::max(a.part_even, b.part_even);
-        md.part_odd = p->part_floats = (p->part_floats + 3) & ~int64_t(3);
-        p->part_floats += std::max({a.part_odd, b.part_odd, int64_t(og.nstrip) * md.n * md.r});
-        p->tiles_cap += std::max(a.ntiles, b.ntiles);
-        p->slots_cap += std::max(a.nstrip, b.nstrip);
-        p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
-        int64_t cap = fin_geometry(md.n, md.m, fin_form(p->rbucket, true), p->fin_elems_lds).ntiles;
-        for (int sc = 0; sc <= 5; ++sc)  // any segment cap set_vec may pick
-            cap = std::max(cap, fin_geometry(md.n, md.m, fin_form(p->rbucket, false), p->fin_elems, sc).ntiles);
-        p->tiles_fin_cap += cap;
-        if (i == 0 || p->mats[i - 1].group != md.group) {
-            p->grng_even.push_back(int32_t(p->red_even.size()));
-            p->grng_even.push_back(0);
-            p->grng_odd.push_back(int32_t(p->red_odd.size()));
-            p->grng_odd.push_back(0);
-        }
-        // fp32/bf16: 4 elements per lane unless an element has more than kRedWide partials
-        // (any geometry set_vec may pick), whose 4-wide item would be one CU's bandwidth
-        const int np_even = std::max(a.nchunk, b.nchunk);
-        const int np_odd = std::max({a.nstrip, b.nstrip, og.nstrip});
-        const int pe = p->f64() || np_even > kRedWide ? 1 : 4, po = p->f64() || np_odd > kRedWide ? 1 : 4;
-        p->red_even_b.push_back(int32_t(p->red_even.size()));
-        for (int64_t s = 0; s < md.m * md.r; s += 64 * pe) p->red_even.push_back(RedItem{int32_t(i), int32_t(s), pe});
-        p->red_even_e.push_back(int32_t(p->red_even.size()));
-        for (int64_t s = 0; s < md.n * md.r; s += 64 * po) p->red_odd.push_back(RedItem{int32_t(i), int32_t(s), po});
-        p->grng_even.back() = int32_t(p->red_even.size());
-        p->grng_odd.back() = int32_t(p->red_odd.size());
-    }
+    // capacities of every list set_vec may build (either vector width, up to kMaxBuckets
+    // buckets): tiles, segments, reduction items, partial slabs
+    int64_t total = 0, strips_max = 0, strip_elems = 0, red_even_cap = 0, red_odd_cap = 0, part_odd_cap = 0, wr_max = 0;
     for (size_t i = 0; i < p->mats.size(); ++i) {
         const MatDesc& md = p->mats[i];
-        const Geom a = geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems);
-        const Geom b = geometry(md.n, md.m, md.r, 0, p->tile_elems);
-        if (i == 0 || p->mats[i - 1].group != md.group) {
-            p->grng_ss0.push_back(int32_t(p->ss0_slots));
-            p->grng_ss0.push_back(0);
+        total += md.n * md.m;
+        const OddGeom og = odd_geometry(md.n, md.m, p->tile_elems);
+        int64_t ns = 0, se = 0, re = 0, po = og.nstrip;
+        for (int v : {p->base_vec[i], 0}) {
+            const Geom g = geometry(md.n, md.m, md.r, v, p->tile_elems);
+            const int64_t W = int64_t(g.lanes) * (v ? 4 : 1);
+            ns = std::max<int64_t>(ns, g.nstrip);
+            se = std::max<int64_t>(se, g.nstrip * (W * md.r + 3));
+            re = std::max<int64_t>(re, (md.m * md.r + 63) / 64 + g.nstrip);
+            po = std::max<int64_t>(po, g.nstrip);
+            wr_max = std::max<int64_t>(wr_max, W * md.r + 3);
         }
-        p->ss0_base.push_back(int32_t(p->ss0_slots));
-        p->ss0_slots += std::max(a.nchunk, b.nchunk);  // unused slots stay zero (bind)
-        p->grng_ss0.back() = int32_t(p->ss0_slots);
+        p->tiles_cap += std::max(geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems).ntiles,
+                                 geometry(md.n, md.m, md.r, 0, p->tile_elems).ntiles);
+        p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
+        int64_t cap = 0;
+        for (int sc = 0; sc <= 5; ++sc)  // any segment cap set_vec may pick
+            cap = std::max(cap, fin_geometry(md.n, md.m, p->rbucket, p->fin_elems, sc).ntiles);
+        p->tiles_fin_cap += cap;
+        strips_max += ns;
+        strip_elems += se;
+        red_even_cap += re;
+        red_odd_cap += (md.n * md.r + 63) / 64;
+        part_odd_cap += po * md.n * md.r + 3;
     }
-    if (p->f64())
-        p->set_f64_tiles();  // fp64: its own kernels and tiles (psgd_f64.hip), no fused forms
-    else
-        p->set_vec(p->base_vec);
+    {
+        const int64_t nb = std::min<int64_t>(kMaxBuckets, int64_t(p->groups.size()));
+        const int64_t wg = std::min<int64_t>(int64_t(p->even_wpc) * kCUs, total / p->even_min + 1);
+        // segments beyond one per strip: one per workgroup boundary (strip walk), up to two per
+        // workgroup (row blocks across strips, ragged strips)
+        const int64_t extra = 2 * nb * wg;
+        p->segs_cap = strips_max + extra;
+        p->ss0_cap = int64_t(p->mats.size()) + extra;
+        p->even_part_cap = strip_elems + extra * wr_max;
+        p->red_even_cap = red_even_cap;
+        p->red_odd_cap = red_odd_cap;
+    }
     // folded orthonormalisation (projection form): every Q unit one panel of rbucket columns
     p->qfold_ok = !p->f64() && (p->rbucket == 2 || p->rbucket == 4) && !p->units_q.empty() &&
                   env_int("PSGD_QFOLD", 1) != 0;
     for (const OrthUnit& u : p->units_q) p->qfold_ok = p->qfold_ok && u.r == p->rbucket && u.count == 1;
-    if (p->qfold_ok) {
-        for (const OrthUnit& u : p->units_q) {
-            int32_t b = -1, e = -1;
-            for (size_t i = 0; i < p->mats.size(); ++i)
-                if (p->mats[i].qoff == u.off) {
-                    b = p->red_even_b[i];
-                    e = p->red_even_e[i];
-                }
-            p->qfold_ok = p->qfold_ok && b >= 0;
-            p->uitems.push_back(b);
-            p->uitems.push_back(e);
-        }
+    const int64_t part_cap = part_odd_cap + 4 + p->even_part_cap;
+    if (p->f64()) {
+        p->set_f64_tiles();  // fp64: its own kernels and tiles (psgd_f64.hip), no fused forms
+        p->red_even_cap = std::max<int64_t>(p->red_even_cap, int64_t(p->red_even.size()));
+    } else {
+        p->set_vec(p->base_vec);
     }
 
     size_t off = 0;
@@ -1037,8 +1109,10 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_tiles_ov = carve(size_t(p->tiles_cap) * sizeof(Tile));
     p->o_tiles_om = carve(size_t(std::max<int64_t>(p->tiles_om_cap, 1)) * sizeof(Tile));
     p->o_tiles_fin = carve(size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(Tile));
-    p->o_red_even = carve(p->red_even.size() * sizeof(RedItem));
-    p->o_red_odd = carve(p->red_odd.size() * sizeof(RedItem));
+    p->o_segs = carve(size_t(std::max<int64_t>(p->segs_cap, 1)) * sizeof(Seg));
+    p->o_wg_seg = carve((size_t(kMaxBuckets) * kEvenWgMax + 1) * sizeof(int32_t));
+    p->o_red_even = carve(size_t(std::max<int64_t>(p->red_even_cap, 1)) * sizeof(RedItem));
+    p->o_red_odd = carve(size_t(std::max<int64_t>(p->red_odd_cap, 1)) * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
     p->o_units_q = carve(p->units_q.size() * sizeof(OrthUnit));
     for (const MatDesc& md : p->mats) {
@@ -1051,30 +1125,22 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_rq = carve(size_t(std::max<int64_t>(p->fmax, 1)) * sizeof(float));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
-    p->o_grng_even = carve(p->grng_even.size() * sizeof(int32_t));
-    p->o_grng_odd = carve(p->grng_odd.size() * sizeof(int32_t));
-    p->ss_stride = std::max(p->red_even.size(), p->red_odd.size());
-    p->o_ss = carve(2 * p->ss_stride * sizeof(float));
-    p->o_grng_fin = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
-    p->o_cnt = carve(size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(int32_t));
-    p->o_gcnt = carve(std::max<size_t>(p->groups.size(), 1) * sizeof(int32_t));
-    p->o_ss_strip = carve(2 * size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(float));
-    p->o_grng_strip = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
-    p->o_gdesc = carve(std::max<size_t>(p->groups.size(), 1) * sizeof(GroupDesc));
-    p->o_ss_fin = carve(2 * size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(float));
-    p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float));
-    p->o_ss0_base = carve(std::max<size_t>(p->ss0_base.size(), 1) * sizeof(int32_t));
-    p->o_grng_ss0 = carve(std::max<size_t>(p->grng_ss0.size(), 1) * sizeof(int32_t));
+    p->o_grng_even = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->o_grng_odd = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->ss_stride = size_t(std::max<int64_t>(p->red_even_cap, p->red_odd_cap));
+    p->o_ss = carve(2 * std::max<size_t>(p->ss_stride, 1) * sizeof(float));
+    p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_cap, 1)) * sizeof(float));
+    p->o_grng_ss0 = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
     p->o_hist = carve(size_t(3) * iters * size_t(p->fmax) * (p->f64() ? sizeof(double) : sizeof(float)));
     p->o_f64_even = carve(std::max<size_t>(p->f64_even.size(), 1) * sizeof(Tile));
     p->o_f64_odd = carve(std::max<size_t>(p->f64_odd.size(), 1) * sizeof(Tile));
     p->o_f64_apply = carve(std::max<size_t>(p->f64_apply.size(), 1) * sizeof(Tile));
     p->o_f64_partoff = carve(std::max<size_t>(p->f64_part_off.size(), 1) * sizeof(int64_t));
     p->o_f64_part = carve(size_t(std::max<int64_t>(p->f64_part, 1)) * sizeof(double));
-    p->o_part = carve(size_t(p->part_floats) * sizeof(float));
+    p->o_part = carve(size_t(part_cap) * sizeof(float));
     if (p->qfold_ok) {
-        p->o_gram = carve(p->red_even.size() * kGramStride * sizeof(double));
-        p->o_uitems = carve(p->uitems.size() * sizeof(int32_t));
+        p->o_gram = carve(size_t(p->red_even_cap) * kGramStride * sizeof(double));
+        p->o_uitems = carve(2 * p->units_q.size() * sizeof(int32_t));
     }
     p->ws_bytes = off;
     *out_plan = p;
@@ -1143,31 +1209,16 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     p->P = static_cast<float*>(P);  // fp64 plans: double buffers (see P64/Q64)
     p->Q = static_cast<float*>(Q);
     p->ws = static_cast<char*>(workspace);
-    p->drop_graphs();
     const size_t nt = p->shapes.size();
     p->grad_tab.bind(p->dev<char>(p->o_ptrs), nt);
     p->rdst_tab.bind(p->dev<char>(p->o_rdst), nt);
     p->odst_tab.bind(p->dev<char>(p->o_odst), nt);
     if (int st = p->upload_tiles()) return st;
-    if (int st = upload(p->dev<void>(p->o_red_even), p->red_even.data(), p->red_even.size() * sizeof(RedItem))) return st;
-    if (int st = upload(p->dev<void>(p->o_red_odd), p->red_odd.data(), p->red_odd.size() * sizeof(RedItem))) return st;
     if (int st = upload(p->dev<void>(p->o_units_p), p->units_p.data(), p->units_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_munits_p), p->munits_p.data(), p->munits_p.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_munits_q), p->munits_q.data(), p->munits_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
-    if (p->qfold_ok)
-        if (int st = upload(p->dev<void>(p->o_uitems), p->uitems.data(), p->uitems.size() * sizeof(int32_t))) return st;
-    if (int st = upload(p->dev<void>(p->o_grng_even), p->grng_even.data(), p->grng_even.size() * sizeof(int32_t))) return st;
-    if (int st = upload(p->dev<void>(p->o_grng_odd), p->grng_odd.data(), p->grng_odd.size() * sizeof(int32_t))) return st;
-    if (int st = upload(p->dev<void>(p->o_ss0_base), p->ss0_base.data(), p->ss0_base.size() * sizeof(int32_t))) return st;
-    if (int st = upload(p->dev<void>(p->o_grng_ss0), p->grng_ss0.data(), p->grng_ss0.size() * sizeof(int32_t))) return st;
-    PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_slots, 1)) * sizeof(float)));
-    // tickets of the folded reduction start at zero (each last arriver resets its own)
-    PSGD_HIP(hipMemset(p->dev<void>(p->o_cnt), 0, size_t(std::max<int64_t>(p->slots_cap, 1)) * sizeof(int32_t)));
-    PSGD_HIP(hipMemset(p->dev<void>(p->o_gcnt), 0, std::max<size_t>(p->groups.size(), 1) * sizeof(int32_t)));
-    // opt-in: the in-launch seam measured slower than the k_reduce boundary it replaces on
-    // every BASELINE config (profiles/r02/fold_ab.txt; cdna_hip_programming.md §5.6 agrees)
-    p->fold = env_int("PSGD_FOLD", 0) != 0;
+    PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_cap, 1)) * sizeof(float)));
     if (p->f64()) {
         if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
         if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
@@ -1332,24 +1383,12 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (nunits > 0) PSGD_HIP(launch_orth(oa, nunits, p->rbucket, even ? p->panel_p : p->panel_q, p->orth_chol, s));
     }
 
-    const bool fprod = p->fin_prod(step, it, fuse);
-    const bool prev_fprod = it > 0 && p->fin_prod(step, it - 1, fuse);
-    const int64_t fin_stride = std::max<int64_t>(p->tiles_fin_cap, 1);
-    const int64_t slot_stride = std::max<int64_t>(p->slots_cap, 1);
-    // even iterations fold their partial reduction into the product (no k_reduce launch)
-    const bool fold = p->fold && even;
-    const bool prev_fold = it > 0 && p->fold && p->even(step, it - 1);
-    // where the previous iteration's reduction left the per-slot sums of squares of its
-    // out-factor (this iteration's raw in-factor) and the per-group slot ranges
-    const float* prev_ss = prev_fold    ? p->dev<float>(p->o_ss_strip) + size_t((it - 1) & 1) * slot_stride
-                           : prev_fprod ? p->dev<float>(p->o_ss_fin) + size_t((it - 1) & 1) * fin_stride
-                                        : ss + size_t((it - 1) & 1) * p->ss_stride;
-    const int32_t* prev_grng = prev_fold    ? p->dev<int32_t>(p->o_grng_strip)
-                               : prev_fprod ? p->dev<int32_t>(p->o_grng_fin)
-                                            : p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
-    if ((it == p->iters - 1 && p->fused_final(step, write_out)) || fprod) {
-        // last iteration, odd: product + residual (+ output at world size 1) in one pass;
-        // fprod: an earlier odd iteration, product only
+    // where the previous iteration's reduction left the per-item sums of squares of its
+    // out-factor (this iteration's raw in-factor) and the per-group item ranges
+    const float* prev_ss = ss + size_t((it - 1) & 1) * p->ss_stride;
+    const int32_t* prev_grng = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
+    if (it == p->iters - 1 && p->fused_final(step, write_out)) {
+        // last iteration, odd: product + residual (+ output at world size 1) in one pass
         FinalArgs fa{};
         fa.mats = p->dev<MatDesc>(p->o_mats);
         fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
@@ -1358,10 +1397,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
         fill_terms(p, step, it, fa.res);
         fa.nres = it;
-        fa.write_out = (write_out && !fprod) ? 1 : 0;
-        fa.product_only = fprod ? 1 : 0;
-        if (fprod && fused_norm(p, fuse, it + 1))
-            fa.ss_out = p->dev<float>(p->o_ss_fin) + size_t(it & 1) * fin_stride + sp.fin[0];
+        fa.write_out = write_out ? 1 : 0;
         fa.yloc = p->hist(1, it);
         fa.state = out;
         if (fused) {
@@ -1374,71 +1410,36 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (proj) {  // no error-feedback terms: P_0 and R' only
             fa.proj_p0 = p->hist(0, 0);
             fa.proj_r = p->dev<float>(p->o_rq);
-
             fill_terms(p, step, 0, fa.res);
             fa.nres = kFinProj;
         }
         fa.ntiles = nfin;
-        if (fl && write_out && !fprod) fa.flat = *fl;  // uncompressed tensors ride in the same launch
+        if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         if (nfin + fa.flat.nitems == 0) return PSGD_OK;
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-        if (!fprod)  // benchmark timing covers the final pass only
-            if (int st = timing_begin(p, s, &ev)) return st;
-        if (p->fin_lds)
-            PSGD_HIP(launch_final_lds(p->dtype, p->rbucket, it, p->fin_smax, p->fin_lds_bytes, fa, nfin, s));
-        else
-            PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, fa.nres, fin_bucket(p->fin_smax), fa, nfin, s));
+        if (int st = timing_begin(p, s, &ev)) return st;  // benchmark timing: the final pass
+        PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, fa.nres, fin_bucket(p->fin_smax), fa, nfin, s));
         if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
         return PSGD_OK;
     }
 
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
-    pa.tiles = p->dev<Tile>(p->o_tiles) + sp.tiles[0];
     pa.grads = p->grad_tab.table();
     pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
-    if (fused0 && !fold) {
-        pa.ss0 = p->dev<float>(p->o_ss0);
-        pa.ss0_base = p->dev<int32_t>(p->o_ss0_base);
-    }
-    if (fold) {
-        pa.fold = 1;
-        pa.cnt = p->dev<int32_t>(p->o_cnt);
-        pa.gcnt = p->dev<int32_t>(p->o_gcnt);
-        pa.groups = p->dev<GroupDesc>(p->o_gdesc);
-        pa.yloc = p->hist(1, it);
-        pa.state = out;
-        if (fused0) {  // the raw state P's joint norm; the group's last strip normalises P
-            pa.norm = 2;
-            pa.raw_in = in;
-            pa.xstate = in;
-            pa.hx = p->hist(0, it);
-        } else if (fused) {
-            pa.norm = 1;
-            pa.ss_in = prev_ss;
-            pa.grng_in = prev_grng;
-            pa.raw_in = p->hist(1, it - 1);
-            pa.xstate = in;
-            pa.hx = p->hist(0, it);
-        }
-        if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters)
-            pa.ss_out = p->dev<float>(p->o_ss_strip) + size_t(it & 1) * slot_stride;
-    }
+    if (fused0) pa.ss0 = p->dev<float>(p->o_ss0);
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
     if (even) {
-        const int nt = sp.tiles[1] - sp.tiles[0];
-        // wave tiles (opt-in A/B knob): no LDS reduction / barrier in the tile epilogue
-        static const bool wave_tiles = env_int("PSGD_PROD_WAVE", 0) != 0;
-        pa.wave_tiles = (wave_tiles && !fold) ? 1 : 0;
-        pa.ntiles = nt;
-        if (nt > 0) PSGD_HIP(launch_product(p->dtype, p->rbucket, true, it, pa, nt, s));
-        if (fold) return PSGD_OK;  // the last tile of each strip reduced it
+        // persistent k_even: this span's workgroups [wg[0], wg[1]) of the segmentation
+        pa.segs = p->dev<Seg>(p->o_segs);
+        pa.wg_seg = p->dev<int32_t>(p->o_wg_seg) + sp.wg[0];
+        PSGD_HIP(launch_even(p->dtype, p->rbucket, it, pa, sp.wg[1] - sp.wg[0], s));
     } else {
         if (sp.ov[1] > sp.ov[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov) + sp.ov[0];
-            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, it, pa, sp.ov[1] - sp.ov[0], s));
+            PSGD_HIP(launch_product_odd(p->dtype, p->rbucket, it, pa, sp.ov[1] - sp.ov[0], s));
         }
         if (sp.om[1] > sp.om[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_om) + sp.om[0];
@@ -1554,17 +1555,16 @@ int psgd_plan_set_buckets(psgd_plan* p, int32_t nbuckets, const int32_t* group_e
         prev = group_end[b];
     }
     if (nbuckets > 0 && prev != ng) return fail(PSGD_ERR_VALUE, "the last bucket must end at the last group");
+    if (nbuckets > kMaxBuckets) return fail(PSGD_ERR_VALUE, "at most 8 buckets");
     DevScope scope(p->device);
     if (p->bound) PSGD_HIP(hipDeviceSynchronize());  // the tile tables are rewritten below
-    p->drop_graphs();
     p->bucket_gend.assign(group_end, group_end + nbuckets);
     p->spans.clear();
     if (!p->f64()) {
-        p->set_vec(p->vec_now);  // matrix-ordered tile lists (PSGD_SORT_TILES is off with buckets)
+        p->set_vec(p->vec_now);  // per-bucket segmentation of the even product, spans
         if (p->bound)
             if (int st = p->upload_tiles()) return st;
     }
-    if (!p->bucket_gend.empty()) p->build_spans();
     return PSGD_OK;
 }
 
@@ -1705,12 +1705,13 @@ int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, 
     }
     pa.nres = nterms;
     if (!odd) {
-        pa.tiles = p->dev<Tile>(p->o_tiles);
-        PSGD_HIP(launch_product(p->dtype, p->rbucket, true, nterms, pa, int(p->tiles.size()), s));
+        pa.segs = p->dev<Seg>(p->o_segs);
+        pa.wg_seg = p->dev<int32_t>(p->o_wg_seg);
+        PSGD_HIP(launch_even(p->dtype, p->rbucket, nterms, pa, int(p->wg_seg.size()) - 1, s));
     } else {
         if (!p->tiles_ov.empty()) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov);
-            PSGD_HIP(launch_product(p->dtype, p->rbucket, false, nterms, pa, int(p->tiles_ov.size()), s));
+            PSGD_HIP(launch_product_odd(p->dtype, p->rbucket, nterms, pa, int(p->tiles_ov.size()), s));
         }
         if (!p->tiles_om.empty()) {
             pa.tiles = p->dev<Tile>(p->o_tiles_om);
@@ -1933,122 +1934,12 @@ int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world
     return PSGD_OK;
 }
 
-// One world-size-1 step: all buckets at once, or (overlap) bucket b on side stream b % 2,
-// forked from and joined back into `s` with events (legal inside a stream capture).
-static int run_step(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s, const FlatArgs* fl) {
-    if (!p->overlap || p->spans.size() < 2) return aggregate_impl(p, grads, out, step, s, fl);
-    for (int i = 0; i < 2; ++i)
-        if (!p->side[i]) PSGD_HIP(hipStreamCreateWithFlags(&p->side[i], hipStreamNonBlocking));
-    if (!p->ev_fork) {
-        PSGD_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-        for (int i = 0; i < 2; ++i) PSGD_HIP(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
-    }
-    PSGD_HIP(hipEventRecord(p->ev_fork, s));
-    for (int i = 0; i < 2; ++i) PSGD_HIP(hipStreamWaitEvent(p->side[i], p->ev_fork, 0));
-    for (size_t b = 0; b < p->spans.size(); ++b)
-        if (int st = aggregate_impl(p, grads, out, step, p->side[b % 2], b == 0 ? fl : nullptr, &p->spans[b])) return st;
-    for (int i = 0; i < 2; ++i) {
-        PSGD_HIP(hipEventRecord(p->ev_join[i], p->side[i]));
-        PSGD_HIP(hipStreamWaitEvent(s, p->ev_join[i], 0));
-    }
-    return PSGD_OK;
-}
-
 // World-size-1 entry (psgd_aggregate / psgd_aggregate_flat): the pointer tables are selected
-// (or uploaded) on the caller's stream first, then the step runs as a replayed HIP graph keyed
-// by everything its launches bake in, on the plan's own stream between two events (the caller's
-// stream may be the legacy default stream, which cannot be captured).
+// (or uploaded) on the caller's stream, then the step's launches follow on it.
 static int aggregate_entry(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
-                           const FlatArgs* fl, const psgd_flat* f) {
-    // the pointer tables are selected (uploaded) on the caller's stream before any fork or capture:
-    // the side streams and the graph then only ever hit
+                           const FlatArgs* fl, const psgd_flat*) {
     if (int st = refresh_pointers(p, grads, s)) return st;
-    const bool graph = p->use_graphs && !p->timing && !p->f64();
-    if (!graph) return run_step(p, grads, out, step, s, fl);
-    const uint64_t key[6] = {uint64_t(p->grad_tab.cur), uint64_t(reinterpret_cast<uintptr_t>(out)),
-                             uint64_t(reinterpret_cast<uintptr_t>(fl ? fl->flat : nullptr)),
-                             uint64_t(fl && f ? f->tab.cur : -1), uint64_t((step * p->iters) & 1),
-                             uint64_t(p->overlap ? 1 : 0)};
-    if (!p->gstream) {
-        PSGD_HIP(hipStreamCreateWithFlags(&p->gstream, hipStreamNonBlocking));
-        PSGD_HIP(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
-        PSGD_HIP(hipEventCreateWithFlags(&p->ev_out, hipEventDisableTiming));
-    }
-    psgd_plan::GraphEntry* ge = nullptr;
-    for (auto& g : p->graphs)
-        if (std::equal(key, key + 6, g.key)) ge = &g;
-    if (!ge) {
-        if (p->graphs.size() >= 16) {  // least recently used goes
-            auto lru = std::min_element(p->graphs.begin(), p->graphs.end(),
-                                        [](const auto& a, const auto& b) { return a.stamp < b.stamp; });
-            (void)hipGraphExecDestroy(lru->exec);
-            p->graphs.erase(lru);
-        }
-        hipGraph_t g = nullptr;
-        PSGD_HIP(hipStreamBeginCapture(p->gstream, hipStreamCaptureModeThreadLocal));
-        const int st = run_step(p, grads, out, step, p->gstream, fl);
-        const hipError_t e = hipStreamEndCapture(p->gstream, &g);
-        if (st) {
-            if (g) (void)hipGraphDestroy(g);
-            return st;
-        }
-        if (e != hipSuccess) return fail(PSGD_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-        psgd_plan::GraphEntry ne{};
-        std::copy(key, key + 6, ne.key);
-        const hipError_t ie = hipGraphInstantiate(&ne.exec, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        if (ie != hipSuccess) return fail(PSGD_ERR_DEVICE, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
-        p->graphs.push_back(ne);
-        ge = &p->graphs.back();
-    }
-    ge->stamp = ++p->graph_clock;
-    PSGD_HIP(hipEventRecord(p->ev_in, s));
-    PSGD_HIP(hipStreamWaitEvent(p->gstream, p->ev_in, 0));
-    PSGD_HIP(hipGraphLaunch(ge->exec, p->gstream));
-    PSGD_HIP(hipEventRecord(p->ev_out, p->gstream));
-    PSGD_HIP(hipStreamWaitEvent(s, p->ev_out, 0));
-    return PSGD_OK;
-}
-
-int psgd_plan_set_graphs(psgd_plan* p, int32_t graphs, int32_t overlap) {
-    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
-    DevScope scope(p->device);
-    if (p->bound && !p->graphs.empty()) PSGD_HIP(hipDeviceSynchronize());
-    p->drop_graphs();
-    p->use_graphs = graphs != 0;
-    p->overlap = overlap != 0;
-    return PSGD_OK;
-}
-
-int psgd_plan_prepare(psgd_plan* p, void* const* grads, void* stream) {
-    if (!p || !grads) return fail(PSGD_ERR_VALUE, "null argument");
-    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
-    DevScope scope(p->device);
-    return refresh_pointers(p, grads, static_cast<hipStream_t>(stream));
-}
-
-int psgd_aggregate_bucket(psgd_plan* p, void* const* grads, void* out, int64_t step, int32_t bucket, psgd_flat* f,
-                          void* const* unc, void* flat_out, void* stream) {
-    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
-    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
-    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
-    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
-    psgd_plan::Span sp;
-    if (int st = bucket_span(p, bucket, &sp)) return st;
-    DevScope scope(p->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (f && f->total > 0) {
-        if (!unc || !flat_out) return fail(PSGD_ERR_VALUE, "null argument");
-        if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
-        if (f->dtype != p->dtype || f->device != p->device) {
-            if (int st = aggregate_impl(p, grads, out, step, s, nullptr, &sp)) return st;
-            return psgd_flat_pack(f, unc, flat_out, 1, stream);
-        }
-        FlatArgs a;
-        if (int st = flat_args(f, unc, flat_out, 1, s, &a)) return st;
-        return aggregate_impl(p, grads, out, step, s, &a, &sp);
-    }
-    return aggregate_impl(p, grads, out, step, s, nullptr, &sp);
+    return aggregate_impl(p, grads, out, step, s, fl);
 }
 
 int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f,

@@ -1703,20 +1703,17 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, bool 
 }
 
 // ---------------------------------------------------------------- partial reduction
-// Sums the partials of each factor element in a FIXED order (row chunks for even
-// iterations, column strips for odd ones): bitwise reproducible, no atomics.
+// Sums the partials of each factor element in a FIXED order (the even product's segments down
+// a column strip, the odd product's column strips): bitwise reproducible, no atomics.
 
-// One item = 64 * per consecutive elements of one factor (per = 4, or 1 for factors with
-// many partials: RedItem::per). per = 4: one 16-byte load per partial when the factor length
-// and its partial slab are 16-byte aligned (lane l owns elements 4l .. 4l+3), else four
-// 256-byte wave loads (lane l owns l, l+64, l+128, l+192). Wave w adds the partials
-// [w*np/4, (w+1)*np/4) of each element in order, then wave 0 adds the four wave sums in
-// order: every element is summed in the same fixed order on every run, whatever the layout.
-// (Four times fewer workgroups than one element per lane: the whole ResNet-50 reduction is
-// resident at once instead of taking two rounds of descriptor + partial round trips.)
-__device__ __forceinline__ int64_t red_elem(bool vec, int64_t start, int lane, int j) {
-    return vec ? start + 4 * lane + j : start + lane + 64 * j;
-}
+// One item = up to 64 * per consecutive elements of one factor (per = 4, or 1 for factors with
+// many partials: RedItem::per) with one partial layout (RedItem::pbase / pstride / np).
+// per = 4: one 16-byte load per partial when the item's partial runs are 16-byte aligned (lane
+// l owns elements 4l .. 4l+3), else four 256-byte wave loads (lane l owns l, l+64, l+128,
+// l+192). Wave w adds the partials [w*np/4, (w+1)*np/4) of each element in order, then wave 0
+// adds the four wave sums in order: every element is summed in the same fixed order on every
+// run, whatever the layout.
+__device__ __forceinline__ int red_elem(bool vec, int lane, int j) { return vec ? 4 * lane + j : lane + 64 * j; }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     __shared__ float red[kWaves * kRedItem];
@@ -1725,19 +1722,18 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         if (wave != 0) return;
         const RedItem it = a.nitems[blockIdx.x - a.nmain];
         const MatDesc d = a.mats[it.mat];
-        const int64_t len = (a.even ? d.n : d.m) * d.r;
-        const int64_t base = a.even ? d.poff : d.qoff;
+        const int64_t base = (a.even ? d.poff : d.qoff) + it.start;
         float x[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {  // in flight together with the norm's loads
-            const int64_t e = red_elem(false, it.start, lane, j);
-            x[j] = a.raw[base + (e < len ? e : 0)];
+            const int e = red_elem(false, lane, j);
+            x[j] = a.raw[base + (e < it.cnt ? e : 0)];
         }
         const float dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t e = red_elem(false, it.start, lane, j);
-            if (j < it.per && e < len) {
+            const int e = red_elem(false, lane, j);
+            if (j < it.per && e < it.cnt) {
                 const float v = x[j] / dn;  // matrix.div_(max(norm, eps))
                 a.xstate[base + e] = v;
                 a.hx[base + e] = v;
@@ -1747,11 +1743,10 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     }
     const RedItem it = a.items[blockIdx.x];
     const MatDesc d = a.mats[it.mat];
-    const int64_t len = (a.even ? d.m : d.n) * d.r;
-    const int64_t poff = a.even ? d.part_even : d.part_odd;
-    const int per = it.per;
-    const bool vec = per == 4 && ((len | poff) & 3) == 0;  // uniform per workgroup
-    const int np = a.even ? d.nchunk : d.odd_nstrip;
+    const int per = it.per, cnt = it.cnt;
+    const int64_t ps = it.pstride;
+    const bool vec = per == 4 && ((it.pbase | ps | int64_t(cnt)) & 3) == 0;  // uniform per workgroup
+    const int np = it.np;
     const int c0 = wave * np / kWaves, c1 = (wave + 1) * np / kWaves;
     // wave 0's first group-norm loads go out before the partials' (group_norm_ss's order:
     // lane-strided sums from 0, then the wave tree), so the two round trips overlap
@@ -1766,16 +1761,16 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     // loads issued 16 at a time (clamped, unconditional): the partials were just written on
     // other XCDs, so each batch is one MALL round trip
-    const gptr<const float> pb = gconst<float>(a.part) + poff;
+    const gptr<const float> pb = gconst<float>(a.part) + it.pbase;
     if (vec) {
-        const int64_t e0 = red_elem(true, it.start, lane, 0);
-        const gptr<const float> p = pb + (e0 < len ? e0 : 0);
+        const int e0 = red_elem(true, lane, 0);
+        const gptr<const float> p = pb + (e0 < cnt ? e0 : 0);
         constexpr int kB = 16;
         for (int c = c0; c < c1; c += kB) {
             float v[kB][4];
 #pragma unroll
             for (int q = 0; q < kB; ++q) {
-                const v4f x = *(gptr<const v4f>)(p + int64_t(c + q < c1 ? c + q : c0) * len);
+                const v4f x = *(gptr<const v4f>)(p + int64_t(c + q < c1 ? c + q : c0) * ps);
                 v[q][0] = x.x; v[q][1] = x.y; v[q][2] = x.z; v[q][3] = x.w;
             }
 #pragma unroll
@@ -1787,11 +1782,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
                 }
         }
     } else if (per == 4) {
-        int64_t ec[4];
+        int ec[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int64_t e = red_elem(false, it.start, lane, j);
-            ec[j] = e < len ? e : 0;
+            const int e = red_elem(false, lane, j);
+            ec[j] = e < cnt ? e : 0;
         }
         constexpr int kB = 4;
         for (int c = c0; c < c1; c += kB) {
@@ -1799,7 +1794,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
 #pragma unroll
             for (int q = 0; q < kB; ++q)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[q][j] = pb[int64_t(c + q < c1 ? c + q : c0) * len + ec[j]];
+                for (int j = 0; j < 4; ++j) v[q][j] = pb[int64_t(c + q < c1 ? c + q : c0) * ps + ec[j]];
 #pragma unroll
             for (int q = 0; q < kB; ++q)
 #pragma unroll
@@ -1809,13 +1804,12 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
                 }
         }
     } else {
-        const int64_t e = int64_t(it.start) + lane;
-        const gptr<const float> p = pb + (e < len ? e : 0);
+        const gptr<const float> p = pb + (lane < cnt ? lane : 0);
         constexpr int kB = 16;
         for (int c = c0; c < c1; c += kB) {
             float v[kB];
 #pragma unroll
-            for (int q = 0; q < kB; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * len];
+            for (int q = 0; q < kB; ++q) v[q] = p[int64_t(c + q < c1 ? c + q : c0) * ps];
 #pragma unroll
             for (int q = 0; q < kB; ++q) {
                 keep(v[q]);
@@ -1834,7 +1828,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         nv = sqrtf(wave_allsum(ssv));
         nv = nv > 1e-16f ? nv : 1e-16f;
     }
-    const int64_t dbase = a.even ? d.qoff : d.poff;
+    const int64_t dbase = (a.even ? d.qoff : d.poff) + it.start;
     float sq = 0.f;
     float tv[4];
 #pragma unroll
@@ -1844,8 +1838,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         const int o = j * 64 + lane;
         float t = ((red[o] + red[kRedItem + o]) + red[2 * kRedItem + o]) + red[3 * kRedItem + o];
         if (nrm) t = t / nv;  // G^T (x / d) == (G^T x) / d up to rounding
-        const int64_t e = red_elem(vec, it.start, lane, j);
-        if (e < len) {
+        const int e = red_elem(vec, lane, j);
+        if (e < cnt) {
             a.yloc[dbase + e] = t;
             a.state[dbase + e] = t;
             sq = fmaf(t, t, sq);

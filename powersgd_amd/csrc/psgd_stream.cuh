@@ -1,17 +1,16 @@
 // Streaming kernels of the PowerSGD hot path, written for CDNA4 (gfx950, wave64).
 //
-// k_product<EVEN=true> and k_apply walk lane-column tiles: a tile is (matrix, column strip,
-// row chunk) and inside a 256-thread workgroup every lane OWNS V consecutive columns
+// k_apply (and the odd lane-column product) walk lane-column tiles: a tile is (matrix, column
+// strip, row chunk) and inside a 256-thread workgroup every lane OWNS V consecutive columns
 // (V = 4 -> 16-byte fp32 / 8-byte bf16 vector loads) while the 4 waves x RW row phases walk
 // the chunk's rows. A wave-instruction reads L*V*sizeof(T) contiguous bytes of one row
 // (L = lanes per row, up to 64 -> 1 KiB). Q-layout factor values ([m, r], per column) stay
 // in registers for the whole tile; P-layout values ([n, r], per row) are broadcast loads.
 //
-//   k_product<EVEN>   reference powersgd.py:185-202
-//     even: Q = Gk^T P -> per-lane column accumulators, reduced over the workgroup's row
-//           phases (DPP + LDS) into one partial per row chunk.
-//     odd:  P = Gk Q   -> k_odd_mfma (matrix cores, below); the lane-column VALU variant is
-//           kept for matrices without the 16-byte vector layout.
+//   k_product<ODD>    reference powersgd.py:185-202, P = Gk Q: a row layout with a lane
+//     reduce-scatter on full-width strips (r <= 4), lane-column tiles with lane sums on narrow
+//     ones; k_odd_mfma (matrix cores, below) for r 5-16. The even product Q = Gk^T P is the
+//     persistent k_even (psgd_even.cuh).
 //     Gk = G0 - sum_{j<k} P_j Q_j^T is formed ON THE FLY from the untouched gradient (the
 //     reference's baddbmm_, :195-202, element by element), so an iteration reads the
 //     gradient once and writes nothing back.
@@ -141,42 +140,6 @@ __device__ __forceinline__ void ld_factor(gptr<const float> p, int r, float (&v)
                 v[c] = c < r ? v[c] : 0.f;
             }
         }
-    }
-}
-
-// The same through the scalar data cache, for a wave-uniform row (s_load_dwordx4 / dwordx2 /
-// dword): read-only factor rows that every lane of a wave needs, kept off the vector memory
-// pipeline that streams the gradient.
-#define PSGD_C __attribute__((address_space(4)))
-template <int R>
-__device__ __forceinline__ void ld_factor_s(const float* base, int64_t off, int r, float (&v)[R]) {
-    const PSGD_C float* p = (const PSGD_C float*)(base) + off;
-    typedef float v4f_ __attribute__((ext_vector_type(4)));
-    typedef float v2f_ __attribute__((ext_vector_type(2)));
-    if constexpr (R == 1) {
-        v[0] = p[0];
-    } else if constexpr (R % 4 == 0) {
-        if (r == R) {
-#pragma unroll
-            for (int c = 0; c < R; c += 4) {
-                const v4f_ x = *(const PSGD_C v4f_*)(p + c);
-                v[c] = x.x; v[c + 1] = x.y; v[c + 2] = x.z; v[c + 3] = x.w;
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < R; ++c) v[c] = c < r ? p[c] : 0.f;
-        }
-    } else if constexpr (R == 2) {
-        if (r == R) {
-            const v2f_ x = *(const PSGD_C v2f_*)p;
-            v[0] = x.x; v[1] = x.y;
-        } else {
-            v[0] = p[0];
-            v[1] = 0.f;
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < R; ++c) v[c] = c < r ? p[c] : 0.f;
     }
 }
 
@@ -321,29 +284,7 @@ __device__ __forceinline__ TileGeom tile_geom(const MatDesc& d, const Tile& t) {
     return g;
 }
 
-constexpr int kUnroll = 4;  // rows in flight per lane
-// products: rows per batch and whether the next batch is issued before the current one is
-// consumed (software pipeline); build-time knobs for A/B runs (Makefile EXTRA=-D...)
-#ifndef PSGD_PROD_UNROLL
-#define PSGD_PROD_UNROLL 4
-#endif
-#ifndef PSGD_PROD_PIPE
-#define PSGD_PROD_PIPE 0
-#endif
-constexpr int kProdUnroll = PSGD_PROD_UNROLL;
-// even product: wave-uniform in-factor rows through scalar loads (build-time knob for A/B;
-// measured slower at rank 4, 29.1 -> 32.4 us on ResNet-50, neutral at rank 1: off)
-#ifndef PSGD_PROD_SCALAR
-#define PSGD_PROD_SCALAR 0
-#endif
-constexpr bool kProdScalar = PSGD_PROD_SCALAR != 0;
-// DIAGNOSTIC ONLY (timing ablations, wrong results): 1 = no in-factor row loads (constant 1),
-// 2 = no epilogue (no LDS reduction, no partial stores). Never set in a product build.
-#ifndef PSGD_PROD_ABL
-#define PSGD_PROD_ABL 0
-#endif
-constexpr int kProdAbl = PSGD_PROD_ABL;
-constexpr bool kProdPipe = PSGD_PROD_PIPE != 0;
+constexpr int kUnroll = 4;  // rows in flight per lane (k_apply, odd lane-column product)
 
 // ------------------------------------------------- odd product, row layout (VALU) --
 // For full-width strips (256 columns = 64 lanes x 4) and r <= 4: a wave takes 16 rows; each
@@ -519,21 +460,17 @@ __device__ __forceinline__ void odd_rows_tile(const ProductArgs& a, const MatDes
     }
 }
 
-// ------------------------------------------------------------------ product -------
-template <typename T, int R, int K, bool EVEN, int V, bool WT = false>
-__device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc& d, const Tile& t,
-                                             float* lds) {
-    constexpr bool wt = WT;
-    TileGeom g = tile_geom<V>(d, t);
-    if constexpr (wt) {  // wave tile: this wave alone walks the chunk's rows
-        g.stride = 64 / g.L;
-        g.first_row = g.row_begin + g.sub;
-    }
+// ------------------------------------------------- odd product, lane-column tiles --
+// P = Gk Q on strips narrower than 256 columns (or without the vector layout): each lane forms
+// the r partial dots of its V columns of a row; the row's lanes are summed with DPP and the
+// strip's partial of the row is stored by the row's first lane.
+template <typename T, int R, int K, int V>
+__device__ __forceinline__ void odd_cols_tile(const ProductArgs& a, const MatDesc& d, const Tile& t) {
+    const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
     const gptr<const T> G = gconst<T>(a.grads[t.tensor]);
     const int nres = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;  // register-cached terms
-    const gptr<const float> xp_base = gconst<float>(a.x) + d.poff;
     const gptr<const float> xq_base = gconst<float>(a.x) + d.qoff;
 
     float bq[KC][V][R];
@@ -544,69 +481,39 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
             for (int v = 0; v < V; ++v)
                 ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bq[k][v]);
     }
-    float xq[EVEN ? 1 : V][R];
-    if constexpr (!EVEN) {
+    float xq[V][R];
 #pragma unroll
-        for (int v = 0; v < V; ++v) ld_factor<R>(xq_base + (g.ccol + v) * r, r, xq[v]);
-    }
-    float acc[EVEN ? V : 1][R];
-#pragma unroll
-    for (int v = 0; v < (EVEN ? V : 1); ++v)
-#pragma unroll
-        for (int c = 0; c < R; ++c) acc[v][c] = 0.f;
+    for (int v = 0; v < V; ++v) ld_factor<R>(xq_base + (g.ccol + v) * r, r, xq[v]);
 
-    // Software pipeline: batch b+1's gradient rows and factor rows are issued before batch b
-    // is consumed, so a lane keeps 2 x kProdUnroll 16-byte loads in flight. Loads are
-    // unconditional from clamped rows (a batch past the chunk re-reads its first rows, which
-    // hit L2). Cold gradients (HBM latency rather than Infinity-Cache latency) need the depth.
-    struct Batch {
-        float x[kProdUnroll][V];
-        int64_t rc[kProdUnroll];
-        float xpu[EVEN ? kProdUnroll : 1][R];
-        float apu[KC][kProdUnroll][R];
-    };
-    const int64_t step = int64_t(kProdUnroll) * g.stride;
-    auto load = [&](Batch& b, int64_t row) {
+    for (int64_t row = g.first_row; row < g.row_end; row += int64_t(kUnroll) * g.stride) {
+        // the rows' error-feedback factor rows travel with the gradient rows (loaded inside
+        // the row loop they were a chain of dependent round trips per batch)
+        float x[kUnroll][V];
+        int64_t rc[kUnroll];
+        float apu[KC][kUnroll][R];
 #pragma unroll
-        for (int u = 0; u < kProdUnroll; ++u) {
+        for (int u = 0; u < kUnroll; ++u) {
             const int64_t rr = row + u * g.stride;
-            b.rc[u] = rr < g.row_end ? rr : g.row_begin;  // clamped: every load is in range
-            Io<T>::ld(G + b.rc[u] * g.m + g.ccol, b.x[u]);
+            rc[u] = rr < g.row_end ? rr : g.row_begin;  // clamped: every load is in range
+            Io<T>::ld(G + rc[u] * g.m + g.ccol, x[u]);
         }
-        // the rows' factor values (in-factor rows for the even product, error-feedback rows)
-        // travel with the gradient rows (loaded inside the row loop they were a chain of
-        // dependent round trips per batch)
+        if constexpr (K > 0) {
 #pragma unroll
-        for (int u = 0; u < kProdUnroll; ++u) {
-            const int32_t prow = int32_t(b.rc[u]) * r;
-            if constexpr (EVEN && (kProdAbl & 1)) {
+            for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
-                for (int c = 0; c < R; ++c) b.xpu[u][c] = 1.f;
-            } else if constexpr (EVEN) {
-                // full-width strips (64 lanes on one row): the row is wave-uniform, so its
-                // factor values come through the scalar cache (kProdScalar)
-                if (kProdScalar && g.L == 64)
-                    ld_factor_s<R>(a.x, d.poff + __builtin_amdgcn_readfirstlane(prow), r, b.xpu[u]);
-                else
-                    ld_factor<R>(xp_base + prow, r, b.xpu[u]);
-            }
-            if constexpr (K > 0) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, b.apu[k][u]);
-            }
+                for (int k = 0; k < K; ++k)
+                    ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + int32_t(rc[u]) * r, r, apu[k][u]);
         }
-    };
-    auto process = [&](Batch& b, int64_t row) {
 #pragma unroll
-        for (int u = 0; u < kProdUnroll; ++u) {
+        for (int u = 0; u < kUnroll; ++u) {
             const bool valid = g.active && (row + u * g.stride) < g.row_end;
-            const int32_t prow = int32_t(b.rc[u]) * r;
+            const int32_t prow = int32_t(rc[u]) * r;
             // error feedback of the previous iterations, formed on the fly
             for (int k = 0; k < nres; ++k) {
                 float ap[R];
                 if constexpr (K > 0) {
 #pragma unroll
-                    for (int c = 0; c < R; ++c) ap[c] = b.apu[k < KC ? k : 0][u][c];
+                    for (int c = 0; c < R; ++c) ap[c] = apu[k < KC ? k : 0][u][c];
                 } else {
                     ld_factor<R>(gconst<float>(a.res.p[k]) + d.poff + prow, r, ap);
                 }
@@ -619,296 +526,35 @@ __device__ __forceinline__ void product_tile(const ProductArgs& a, const MatDesc
                     } else {
                         ld_factor<R>(gconst<float>(a.res.q[k]) + d.qoff + (g.ccol + v) * r, r, bb);
                     }
-                    b.x[u][v] = b.x[u][v] - dotr<R>(ap, bb);
+                    x[u][v] = x[u][v] - dotr<R>(ap, bb);
                 }
             }
 #pragma unroll
-            for (int v = 0; v < V; ++v) b.x[u][v] = valid ? b.x[u][v] : 0.f;
-            if constexpr (EVEN) {
+            for (int v = 0; v < V; ++v) x[u][v] = valid ? x[u][v] : 0.f;
+            float dot[R];
 #pragma unroll
-                for (int v = 0; v < V; ++v)
+            for (int c = 0; c < R; ++c) {
+                float sacc = x[u][0] * xq[0][c];
 #pragma unroll
-                    for (int c = 0; c < R; ++c) acc[v][c] = fmaf(b.x[u][v], b.xpu[u][c], acc[v][c]);
-            } else {
-                float dot[R];
-#pragma unroll
-                for (int c = 0; c < R; ++c) {
-                    float sacc = b.x[u][0] * xq[0][c];
-#pragma unroll
-                    for (int v = 1; v < V; ++v) sacc = fmaf(b.x[u][v], xq[v][c], sacc);
-                    dot[c] = sum_within(sacc, g.L);
-                }
-                const int64_t rr = row + u * g.stride;
-                if (g.ql == 0 && rr < g.row_end) {
-                    gptr<float> dst = gmut<float>(a.part) + d.part_odd + (int64_t(t.strip) * g.n + rr) * r;
-#pragma unroll
-                    for (int c = 0; c < R; ++c)
-                        if (c < r) dst[c] = dot[c];
-                }
+                for (int v = 1; v < V; ++v) sacc = fmaf(x[u][v], xq[v][c], sacc);
+                dot[c] = sum_within(sacc, g.L);
             }
-        }
-    };
-    if constexpr (kProdPipe || (EVEN && wt)) {
-        Batch cur;
-        load(cur, g.first_row);
-        for (int64_t row = g.first_row; row < g.row_end; row += step) {
-            Batch nxt;
-            // issued before cur is consumed (no keep(): that would wait); none past the chunk
-            // (wave-uniform: a tile's last batch prefetched nothing useful)
-            const bool more = row + step < g.row_end;
-            if (more) load(nxt, row + step);
-            process(cur, row);
-            if (more) cur = nxt;
-        }
-    } else {
-        for (int64_t row = g.first_row; row < g.row_end; row += step) {
-            Batch cur;
-            load(cur, row);
-            process(cur, row);
-        }
-    }
-
-    if constexpr (EVEN && R == 1) {
-        // iteration-0 norm fold: this chunk's share of the raw in-factor's sum of squares
-        // (written before the partial reduction reuses the LDS scratch)
-        if (WT && a.ss0 && t.strip == 0) {  // wave tile: one wave, no barrier
-            float sq = 0.f;
-            for (int64_t row = g.row_begin + g.lane; row < g.row_end; row += 64) {
-                const float x = xp_base[row];
-                sq = fmaf(x, x, sq);
-            }
-            sq = sum_within(sq, 64);
-            if (g.lane == 0) a.ss0[a.ss0_base[t.mat] + t.chunk] = sq;
-        } else if (a.ss0 && t.strip == 0) {
-            float sq = 0.f;
-            for (int64_t row = g.row_begin + threadIdx.x; row < g.row_end; row += kBlock) {
-                const float x = xp_base[row];
-                sq = fmaf(x, x, sq);
-            }
-            sq = sum_within(sq, 64);
-            if ((threadIdx.x & 63) == 0) lds[g.wave] = sq;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const float tot = ((lds[0] + lds[1]) + lds[2]) + lds[3];
-                a.ss0[a.ss0_base[t.mat] + t.chunk] = tot;
-            }
-            __syncthreads();
-        }
-    }
-    if constexpr (EVEN && (kProdAbl & 2)) {
-        float t = 0.f;
+            const int64_t rr = row + u * g.stride;
+            if (g.ql == 0 && rr < g.row_end) {
+                gptr<float> dst = gmut<float>(a.part) + d.part_odd + (int64_t(t.strip) * g.n + rr) * r;
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int c = 0; c < R; ++c) t += acc[v][c];
-        if (t == 1234.5f) a.part[d.part_even] = t;  // keeps the loads alive
-        return;
-    }
-    if constexpr (EVEN) {
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int c = 0; c < R; ++c) acc[v][c] = sum_across(acc[v][c], g.L);  // row phases
-        if constexpr (WT) {  // wave tile: the partials straight from registers (row-phase 0 lanes)
-            if (g.sub == 0) {
-                gptr<float> part = gmut<float>(a.part) + d.part_even + int64_t(t.chunk) * g.m * r;
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    const int64_t col = int64_t(g.col0) + v;
-                    if (g.active && col < g.m) {
-                        if constexpr (R == 4) {
-                            if (r == 4) {
-                                const v4f x = {acc[v][0], acc[v][1], acc[v][2], acc[v][3]};
-                                *(gptr<v4f>)(part + col * 4) = x;
-                                continue;
-                            }
-                        }
-#pragma unroll
-                        for (int c = 0; c < R; ++c)
-                            if (c < r) part[col * r + c] = acc[v][c];
-                    }
-                }
-            }
-            return;
-        }
-        const int width = g.L * V * R;  // floats per wave
-        if (g.sub == 0) {
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-#pragma unroll
-                for (int c = 0; c < R; ++c) lds[g.wave * width + (g.ql * V + v) * R + c] = acc[v][c];
-        }
-        __syncthreads();
-        gptr<float> part = gmut<float>(a.part) + d.part_even + int64_t(t.chunk) * g.m * r;
-        const int64_t col0 = int64_t(t.strip) * g.L * V;
-        // A full strip of an r == R matrix is one contiguous run of `width` partials: 16-byte
-        // plain stores of 4 consecutive sums per thread (the per-element order is unchanged).
-        // The dword write-through stores below cost the epilogue ~5 us per ResNet-50 rank-4
-        // product (one fabric write per dword; ablation in profiles/r02b/ab).
-        const bool vec_out = !a.fold && r == R && (width & 3) == 0 && col0 + g.L * V <= g.m &&
-                             ((d.part_even + int64_t(t.chunk) * g.m * r + col0 * R) & 3) == 0;
-        if (vec_out) {
-            gptr<float> dst = part + col0 * R;
-            for (int i4 = threadIdx.x * 4; i4 < width; i4 += kBlock * 4) {
-                v4f sv = *reinterpret_cast<const v4f*>(lds + i4);
-#pragma unroll
-                for (int w = 1; w < kWaves; ++w) sv += *reinterpret_cast<const v4f*>(lds + w * width + i4);
-                *(gptr<v4f>)(dst + i4) = sv;
-            }
-            return;
-        }
-        for (int idx = threadIdx.x; idx < width; idx += kBlock) {
-            float s = lds[idx];
-#pragma unroll
-            for (int w = 1; w < kWaves; ++w) s += lds[w * width + idx];
-            const int c = idx % R;
-            const int64_t col = col0 + idx / R;
-            if (c < r && col < g.m) {
-                // folded reduction: write-through (sc1) stores, read by the last arriver on
-                // another XCD after an acquire, with no release fence (and L2 write-back) here
-                if (a.fold)
-                    __hip_atomic_store(&part[col * r + c], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else
-                    part[col * r + c] = s;
+                for (int c = 0; c < R; ++c)
+                    if (c < r) dst[c] = dot[c];
             }
         }
     }
 }
 
-// ------------------------------------------------ folded even reduction (epilogue) --
-// Publish this workgroup's stores and take a ticket on `cnt` (cdna_hip_programming.md §5
-// "In-launch split-K reduction": the partial slabs are written through (sc1), so every wave's
-// vmcnt drain + the relaxed agent-scope fetch_add suffice; `release` adds the agent-scope
-// release for plain stores. The last arriver resets the counter for the next launch and
-// acquires before it reads the other workgroups' data). True in the last arriving workgroup.
-__device__ __forceinline__ bool arrive_last(int32_t* cnt, int32_t target, float* lds, bool release) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (release) {  // plain stores to publish; write-through (sc1) stores need no fence
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const int32_t old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = old == target - 1;
-        if (last) {
-            __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        lds[0] = last ? 1.f : 0.f;
-    }
-    __syncthreads();
-    const bool last = lds[0] != 0.f;
-    __syncthreads();  // lds[0] is scratch again
-    return last;
-}
-
-// The last tile of a column strip: sum the strip's partials over the row chunks (fixed order),
-// divide by the in-factor's joint norm, write the out-factor (history + state) and the strip's
-// sum of squares; the last strip of the group writes the normalised in-factor.
-__device__ __forceinline__ void fold_even_strip(const ProductArgs& a, const MatDesc& d, const Tile& t, float* lds) {
-    if (!arrive_last(a.cnt + d.slot0 + t.strip, d.nchunk, lds, false)) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = d.r;
-    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
-    const int64_t c0 = int64_t(t.strip) * W, c1 = d.m < c0 + W ? d.m : c0 + W;
-    const int64_t e0 = c0 * r, e1 = c1 * r, len = d.m * r;
-    const GroupDesc g = a.groups[d.group];
-    float dn = 1.f;
-    if (a.norm == 1) {
-        dn = group_norm_ss(a.ss_in, a.grng_in, d.group);
-    } else if (a.norm == 2) {  // the raw in-factor's joint norm (orthogonalization.py:5-6)
-        // every wave of every reducer of the group: the same lane-strided order, 16 loads in
-        // flight per lane (a dependent chain of single loads cost one MALL round trip each)
-        const int64_t gl = int64_t(g.count) * g.n * g.r;
-        const float* x0 = a.raw_in + g.poff;
-        float acc = 0.f;
-        for (int64_t e0 = lane; e0 < gl; e0 += 64 * 16) {
-            float v[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int64_t e = e0 + int64_t(q) * 64;
-                v[q] = x0[e < gl ? e : 0];
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                keep(v[q]);
-                const float x = e0 + int64_t(q) * 64 < gl ? v[q] : 0.f;
-                acc = fmaf(x, x, acc);
-            }
-        }
-        const float nrm = sqrtf(wave_allsum(acc));
-        dn = nrm > 1e-16f ? nrm : 1e-16f;
-    }
-    const float* part = a.part + d.part_even;
-    constexpr int kB = 16;
-    float ssq = 0.f;
-    for (int64_t e = e0 + tid; e < e1; e += kBlock) {
-        float sum = 0.f;
-        for (int c = 0; c < d.nchunk; c += kB) {  // kB loads in flight (clamped, unconditional)
-            float v[kB];
-#pragma unroll
-            for (int q = 0; q < kB; ++q) v[q] = part[int64_t(c + q < d.nchunk ? c + q : 0) * len + e];
-#pragma unroll
-            for (int q = 0; q < kB; ++q) {
-                keep(v[q]);
-                sum += c + q < d.nchunk ? v[q] : 0.f;
-            }
-        }
-        if (a.norm) sum = sum / dn;  // G^T (x / d) == (G^T x) / d up to rounding
-        a.yloc[d.qoff + e] = sum;
-        a.state[d.qoff + e] = sum;
-        ssq = fmaf(sum, sum, ssq);
-    }
-    if (a.ss_out) {
-        ssq = wave_allsum(ssq);
-        if (lane == 0) lds[1 + wave] = ssq;
-        __syncthreads();
-        if (tid == 0) a.ss_out[d.slot0 + t.strip] = ((lds[1] + lds[2]) + lds[3]) + lds[4];
-    }
-    if (!a.xstate) return;
-    // group ticket: orders the other strips' reads of the raw in-factor before the overwrite
-    if (!arrive_last(a.gcnt + d.group, g.strips, lds, true)) return;
-    // the whole group's strips are reduced (so all of its product tiles are done): the
-    // in-factor may be overwritten with its normalised values (matrix.div_, :6)
-    const int64_t gl = int64_t(g.count) * g.n * g.r;
-    for (int64_t e0 = tid; e0 < gl; e0 += int64_t(kBlock) * 8) {
-        float v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int64_t e = e0 + int64_t(q) * kBlock;
-            v[q] = a.raw_in[g.poff + (e < gl ? e : 0)];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            keep(v[q]);
-            const int64_t e = e0 + int64_t(q) * kBlock;
-            if (e < gl) {
-                const float x = v[q] / dn;
-                a.xstate[g.poff + e] = x;
-                a.hx[g.poff + e] = x;
-            }
-        }
-    }
-}
-
-// PSGD_PROD_WPE (A/B build knob): an occupancy target (waves per SIMD) for the even product
-#ifndef PSGD_PROD_WPE
-#define PSGD_PROD_WPE 1
-#endif
-template <typename T, int R, int K, bool EVEN, bool WT = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EVEN && !WT ? PSGD_PROD_WPE : 1))) void k_product(ProductArgs a) {
-    // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees d.vec == 0)
-    __shared__ float lds[EVEN && !WT ? kWaves * 64 * (R <= 8 ? 4 : 1) * R : 1];
-    int tix = blockIdx.x;
-    if constexpr (WT) {  // wave tiles (even, no fold): wave-uniform exit, no barrier follows
-        tix = int(blockIdx.x) * kWaves + int(threadIdx.x >> 6);
-        if (tix >= a.ntiles) return;
-    }
-    const Tile t = a.tiles[tix];
+template <typename T, int R, int K>
+__global__ __launch_bounds__(kBlock) void k_product_odd(ProductArgs a) {
+    const Tile t = a.tiles[blockIdx.x];
     const MatDesc d = a.mats[t.mat];
-    if constexpr (!EVEN && R <= 4) {
+    if constexpr (R <= 4) {
         if (d.vec && d.lanes == 64) {  // full-width strips: row layout + reduce-scatter
             odd_rows_tile<T, R, K>(a, d, t);
             return;
@@ -916,17 +562,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(EVEN && 
     }
     if constexpr (R <= 8) {
         if (d.vec) {
-            product_tile<T, R, K, EVEN, 4, WT>(a, d, t, lds);
-            if constexpr (EVEN) {
-                if (a.fold) fold_even_strip(a, d, t, lds);
-            }
+            odd_cols_tile<T, R, K, 4>(a, d, t);
             return;
         }
     }
-    product_tile<T, R, K, EVEN, 1, WT>(a, d, t, lds);
-    if constexpr (EVEN) {
-        if (a.fold) fold_even_strip(a, d, t, lds);
-    }
+    odd_cols_tile<T, R, K, 1>(a, d, t);
 }
 
 // ------------------------------------------------------- odd product on MFMA -------
@@ -1341,46 +981,33 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
 
 // ------------------------------------------------------------------ dispatch ------
 template <typename T, int R>
-hipError_t dispatch_product_r(bool even, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
+hipError_t dispatch_odd_r(int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     constexpr bool kCache = R <= 8;
     const int K = (kCache && nres <= 3) ? nres : -1;
-    // wave tiles only for the register-cached instances (ranks <= 8, <= 3 terms)
-    const bool wtl = even && a.wave_tiles && K >= 0;
-    const dim3 grid(wtl ? (ntiles + kWaves - 1) / kWaves : ntiles), block(kBlock);
-#define PSGD_P(KK)                                                                       \
-    do {                                                                                 \
-        if (even && a.wave_tiles && KK >= 0)                                             \
-            k_product<T, R, (KK >= 0 ? KK : 0), true, true><<<grid, block, 0, s>>>(a);   \
-        else if (even)                                                                   \
-            k_product<T, R, KK, true><<<grid, block, 0, s>>>(a);                         \
-        else                                                                             \
-            k_product<T, R, KK, false><<<grid, block, 0, s>>>(a);                        \
-    } while (0)
+    const dim3 grid(ntiles), block(kBlock);
     if constexpr (kCache) {
         switch (K) {
-            case 0: PSGD_P(0); break;
-            case 1: PSGD_P(1); break;
-            case 2: PSGD_P(2); break;
-            case 3: PSGD_P(3); break;
-            default: PSGD_P(-1); break;
+            case 0: k_product_odd<T, R, 0><<<grid, block, 0, s>>>(a); break;
+            case 1: k_product_odd<T, R, 1><<<grid, block, 0, s>>>(a); break;
+            case 2: k_product_odd<T, R, 2><<<grid, block, 0, s>>>(a); break;
+            case 3: k_product_odd<T, R, 3><<<grid, block, 0, s>>>(a); break;
+            default: k_product_odd<T, R, -1><<<grid, block, 0, s>>>(a); break;
         }
     } else {
-        PSGD_P(-1);
+        k_product_odd<T, R, -1><<<grid, block, 0, s>>>(a);
     }
-#undef PSGD_P
     return hipGetLastError();
 }
 
 template <typename T>
-hipError_t dispatch_product(int R, bool even, int nres, const ProductArgs& a, int ntiles,
-                            hipStream_t s) {
+hipError_t dispatch_odd(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     switch (R) {
-        case 1: return dispatch_product_r<T, 1>(even, nres, a, ntiles, s);
-        case 2: return dispatch_product_r<T, 2>(even, nres, a, ntiles, s);
-        case 4: return dispatch_product_r<T, 4>(even, nres, a, ntiles, s);
-        case 8: return dispatch_product_r<T, 8>(even, nres, a, ntiles, s);
-        case 16: return dispatch_product_r<T, 16>(even, nres, a, ntiles, s);
-        case 32: return dispatch_product_r<T, 32>(even, nres, a, ntiles, s);
+        case 1: return dispatch_odd_r<T, 1>(nres, a, ntiles, s);
+        case 2: return dispatch_odd_r<T, 2>(nres, a, ntiles, s);
+        case 4: return dispatch_odd_r<T, 4>(nres, a, ntiles, s);
+        case 8: return dispatch_odd_r<T, 8>(nres, a, ntiles, s);
+        case 16: return dispatch_odd_r<T, 16>(nres, a, ntiles, s);
+        case 32: return dispatch_odd_r<T, 32>(nres, a, ntiles, s);
         default: return hipErrorInvalidValue;
     }
 }

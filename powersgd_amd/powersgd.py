@@ -281,15 +281,6 @@ class BasicPowerSGD(Aggregator):
         self._q_comm: Optional[torch.Tensor] = None
         self._buckets: Optional[List[tuple]] = None  # W > 1: (p_off, p_len, q_off, q_len) per bucket
         self._ipc_open = False  # W > 1 with PSGD_IPC_ALLREDUCE=1: peers' exchange buffers mapped
-        # world size 1: steps replayed as HIP graphs, buckets overlapped on side streams
-        # both opt-in: measured slower on MI355X / ROCm 7.2 (profiles/r02/graphs_overlap): a
-        # graph replay plus the event hop onto the plan's stream costs more than the launches
-        # it replaces, and the side-stream buckets add launches and cross-stream waits
-        self._graphs = os.environ.get("PSGD_GRAPHS", "0") == "1"
-        self._w1_ready = False
-        self._overlap_ok = False
-        self._overlap_on = os.environ.get("PSGD_W1_OVERLAP", "0") == "1"
-        self._plan.set_graphs(self._graphs, False)
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
@@ -329,8 +320,6 @@ class BasicPowerSGD(Aggregator):
         out_ptr = self._slab.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
-        if not self._w1_ready and not is_distributed():
-            self._w1_setup()
         if is_distributed():
             world = torch.distributed.get_world_size()
             iters = self.config.num_iters_per_step
@@ -356,32 +345,6 @@ class BasicPowerSGD(Aggregator):
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
         return outs
-
-    def _w1_setup(self) -> None:
-        """World size 1, first call: cut plans of >= 32 MB with >= 2 shape groups into buckets
-        and let the library run them as independent sub-steps on two side streams inside the
-        step's HIP graph (psgd_plan_set_graphs), so one bucket's latency-bound launches (partial
-        reduction, orthonormalisation) overlap another's streaming passes. Opt-in (PSGD_W1_OVERLAP=1,
-        PSGD_GRAPHS=1): both measured slower than plain launches on MI355X."""
-        self._w1_ready = True
-        big = sum(p.numel() for p in self.params) * self.params[0].element_size() >= (32 << 20)
-        if (big and self.dtype != torch.float64
-                and len(self._plan.groups()) >= 2):
-            if self._buckets is None:
-                self._setup_buckets()
-            self._overlap_ok = len(self._buckets) > 1
-        self._plan.set_graphs(self._graphs, self._overlap_ok and self._overlap_on)
-
-    @property
-    def overlap(self) -> bool:
-        return self._overlap_ok and self._overlap_on
-
-    @overlap.setter
-    def overlap(self, on: bool) -> None:
-        """Benchmarks turn the bucket overlap off to time kernels alone (synchronises)."""
-        self._overlap_on = bool(on)
-        if self._w1_ready:
-            self._plan.set_graphs(self._graphs, self._overlap_ok and self._overlap_on)
 
     def _aggregate_ipc(self, ptrs: int, out_ptr: int, step: int, world: int, stream: int) -> None:
         """Prototype: the LAST iteration's factor all-reduce as a one-shot sum over IPC mappings

@@ -43,7 +43,7 @@ def _rel(a, b, scale):
 
 
 def _make(shapes, rank, iters, dtype=torch.float32, fuse=True, proj=True):
-    env = {"PSGD_FUSE_FINAL": ("2" if fuse is True else str(int(fuse))) if fuse else "0",  # 2, 3 or 0
+    env = {"PSGD_FUSE_FINAL": ("2" if fuse is True else str(int(fuse))) if fuse else "0",  # 2 or 0
            "PSGD_FIN_PROJ": "1" if proj else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
@@ -64,14 +64,12 @@ def _make(shapes, rank, iters, dtype=torch.float32, fuse=True, proj=True):
 NARROW = [s for s in SHAPES if int(torch.tensor(s[1:]).prod()) <= 2048]
 
 
-# mode: PSGD_FUSE_FINAL for the fused plan (2: register panels allowed at every rank, LDS
-# panels where they do not fit; 3: the LDS-panel kernel k_final_lds forced); "2k": mode 2
-# with the projection form off (the K-term form at I = 2)
+# mode: PSGD_FUSE_FINAL for the fused plan (2: the K-term form allowed at every rank); "2k": mode
+# 2 with the projection form off (the K-term form at I = 2)
 @pytest.mark.parametrize("rank,iters,narrow,mode", [
     (1, 2, False, 2), (2, 2, False, 2), (1, 1, False, 2), (2, 1, False, 2), (1, 3, False, 2), (1, 4, False, 2),
     (4, 2, False, 2), (2, 3, False, 2), (1, 3, True, 2), (2, 4, True, 2), (2, 2, True, 2),
-    (4, 2, False, "2k"), (2, 2, False, "2k"), (4, 2, True, 2),
-    (4, 2, False, 3), (2, 2, False, 3), (4, 1, False, 3), (2, 1, True, 3)])
+    (4, 2, False, "2k"), (2, 2, False, "2k"), (4, 2, True, 2), (4, 1, False, 2), (4, 1, True, 2)])
 def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
     shapes = NARROW if narrow else SHAPES
     proj = mode != "2k"
@@ -113,7 +111,7 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
     expect_odd_last = sum(((t * iters + iters - 1) % 2) == 1 for t in range(3))
     projection = proj and mode == 2 and iters == 2 and rank in (2, 4)
-    if narrow or (rank == 1 and iters <= 2) or mode == 3 or projection:  # configurations that must fuse
+    if narrow or (rank == 1 and iters <= 2) or projection:  # configurations that must fuse
         assert n_fused == expect_odd_last, (n_fused, expect_odd_last)
 
 

@@ -62,7 +62,9 @@ def test_multiworker_gloo_on_one_gpu(key):
 def _bucket_worker(rank_id, world, initfile, cfg, steps):
     """ResNet-50 shapes at world size `world`: the bucketed, overlapped collectives (default
     PSGD_BUCKETS = 4, async all-reduce per bucket slice) against the oracle run in the same
-    processes over the same gloo group, and against the single-collective path bitwise."""
+    processes over the same gloo group, and against the single-collective path. The even
+    product's workgroup ranges are cut per bucket (k_even), so the two paths differ in which
+    rows share a partial sum: equal to rounding, not bitwise."""
     import os as _os
 
     from oracle import powersgd_oracle as O
@@ -101,10 +103,9 @@ def _bucket_worker(rank_id, world, initfile, cfg, steps):
                 res_d, res_c = gd, gc
             runs.append((len(psgd._powersgd._buckets), outs_all))
         assert runs[0][0] > 1 and runs[1][0] == 1, (runs[0][0], runs[1][0])
-        if world == 2:  # a SUM of two values does not depend on the order: bitwise equal
-            for a, b in zip(runs[0][1], runs[1][1]):
-                for x, y in zip(a, b):
-                    assert torch.equal(x, y)
+        for t, (a, b) in enumerate(zip(runs[0][1], runs[1][1])):
+            for i, (x, y) in enumerate(zip(a, b)):
+                check(_rel_err(x, y, y), 1e-5 if t == 0 else TOL_FREE, cfg, "buckets-vs-one", rank_id, t, i)
         torch.distributed.barrier()
     finally:
         _os.environ.pop("PSGD_BUCKETS", None)

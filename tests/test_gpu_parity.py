@@ -252,29 +252,44 @@ def test_wide_rank_free_running(rank, iters):
         res_d, res_c = gd, gc
 
 
-@pytest.mark.parametrize("rank,iters,dtype", [(1, 2, torch.float32), (4, 2, torch.float32), (2, 1, torch.float32),
-                                             (2, 3, torch.bfloat16)])
-def test_w1_bucket_overlap_bitwise(rank, iters, dtype):
-    """World size 1, ResNet-50 shapes: the buckets run as independent sub-steps on two side
-    streams inside the step's HIP graph (psgd_plan_set_graphs). Same tiles, same reduction
-    order: the result must be bitwise the one of the single-stream launch sequence, over
-    several steps (alternating parities at I = 1 and 3)."""
+@pytest.mark.parametrize("rank,wpc,emin", [(1, 1, 16384), (4, 4, 1024), (4, 2, 200000), (2, 3, 4096)])
+def test_even_segmentation_forms(rank, wpc, emin):
+    """The persistent even product (k_even) splits the gradient bytes into one range per
+    workgroup (PSGD_EVEN_WPC workgroups per CU, at least PSGD_EVEN_MIN elements each): the setting
+    only moves segment boundaries (which rows share a partial). Every setting matches the oracle
+    per step from the same state, and a rerun from the same state is bitwise identical."""
     shapes = resnet50_shapes()
+    env = {"PSGD_EVEN_WPC": str(wpc), "PSGD_EVEN_MIN": str(emin)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        psgd = PowerSGD([torch.zeros(s, device=DEV) for s in shapes], Config(rank, 2, 2, 0))
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    p0 = psgd._powersgd._ps_buffer.clone()
+    q0 = psgd._powersgd._qs_buffer.clone()
+    grads = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=77)]
+    ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 2, 2, 0)
+    ora.codec.p_flat.copy_(p0.cpu())
+    ora.codec.q_flat.copy_(q0.cpu())
+    gc = [g.clone() for g in grads]
+    oc = O.policy_step(ora, gc)
     runs = []
-    for overlap in (True, False):
-        psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dtype) for s in shapes], Config(rank, 2, iters, 0))
-        psgd._powersgd._graphs = overlap  # the opt-in graph + side-stream mode against plain launches
-        psgd._powersgd.overlap = overlap
-        res = [torch.zeros(s, device=DEV, dtype=dtype) for s in shapes]
-        got = []
-        for t in range(3):
-            grads = [(r + torch.from_numpy(f).to(DEV)).to(dtype) for r, f in zip(res, hash_tensors(shapes, seed=40 + t))]
-            outs = psgd.aggregate(grads)
-            torch.cuda.synchronize()
-            got.append([o.clone() for o in outs] + [g.clone() for g in grads])
-            res = grads
-        assert psgd._powersgd.overlap == overlap
-        runs.append(got)
-    for a, b in zip(runs[0], runs[1]):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
+    for _ in range(2):
+        psgd._powersgd._ps_buffer.copy_(p0)
+        psgd._powersgd._qs_buffer.copy_(q0)
+        psgd.step_counter = psgd._powersgd.step_counter = 0
+        gd = [g.to(DEV) for g in grads]
+        od = psgd.aggregate(gd)
+        torch.cuda.synchronize()
+        runs.append([o.clone() for o in od] + [g.clone() for g in gd] + [psgd._powersgd._qs_buffer.clone()])
+        for i, g in enumerate(grads):
+            tol = TOL_STEP_R1 if rank == 1 else TOL_STEP
+            check(_rel(od[i], oc[i], g), tol, rank, wpc, emin, i, "out")
+            check(_rel(gd[i], gc[i], g), tol, rank, wpc, emin, i, "res")
+    for x, y in zip(runs[0], runs[1]):
+        assert torch.equal(x, y)
