@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--mode", default="both", choices=["both", "cold", "warm"],
                     help="profiling runs: time only one cache state (the headline needs 'both' or 'cold')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N = 1: skip the rank-4 block and the world-size > 1 path block (1-rank RCCL group)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--launch-check", action="store_true",
                     help="rendezvous + world-size report only (no codec; CPU-testable with gloo)")
@@ -201,9 +203,6 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    from powersgd_amd import Config, PowerSGD
-    from powersgd_amd.workloads import CONFIGS
-
     if world > 1:
         # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0
         # over gloo exercises the N > 1 code path end to end; the real run is RCCL, one GPU
@@ -220,14 +219,73 @@ def main():
             print(f"bench.py: process group reports {got} ranks, --gpus {a.gpus}", file=sys.stderr)
             sys.exit(3)
     dev = torch.device("cuda", local)
-    c = dict(CONFIGS[a.config])
-    c["name"] = a.config
-    if a.iters is not None:
+    out = measure(a, a.config, world, rank, dev, backend, a.mode)
+    if rank == 0 and world == 1 and not a.no_extra:
+        # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
+        # world size 1, cold, same steps
+        if a.config != "cfg3_resnet50_r4":
+            r4 = measure(a, "cfg3_resnet50_r4", 1, 0, dev, backend, "cold")
+            out["rank4"] = {k: r4[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
+            out["rank4"]["config"] = r4["config"]
+        # the world-size > 1 code path (bucketed async factor all-reduces, per-bucket kernels,
+        # write-only output pass) timed on this one GPU through a 1-rank RCCL group: the
+        # per-rank compute floor of every multi-GPU point (no xGMI traffic: one rank)
+        out["w_gt1_path"] = one_rank_group(a, dev)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        c = dict(CONFIGS_()[a.config])
+        c["name"] = a.config
+        if a.iters is not None:
+            c["iters"] = a.iters
+        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def CONFIGS_():
+    from powersgd_amd.workloads import CONFIGS
+
+    return CONFIGS
+
+
+def one_rank_group(a, dev):
+    """cfg3 and cfg2 through PowerSGD.aggregate with torch.distributed initialised as ONE RCCL
+    rank on this GPU: is_distributed() is True, so the exact multi-GPU code path runs."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                         device_id=dev)
+    try:
+        res = {"note": "world-size>1 code path on one GPU via a 1-rank RCCL process group (per-rank compute floor; "
+                       "no xGMI traffic)"}
+        for cfg in ("cfg3_resnet50_r4", "cfg2_resnet50_r1"):
+            m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
+            res[cfg] = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
+            res[cfg]["buckets"] = m["config"]["buckets"]
+        return res
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def measure(a, cfg_name, world, rank, dev, backend, mode, dist_path=False):
+    """One workload: warm-up, the timed cold (rotating sets) and warm loops, the final-pass
+    roofline pass. `world` is the job's world size (1 for the 1-rank group)."""
+    from powersgd_amd import Config, PowerSGD
+
+    CONFIGS = CONFIGS_()
+    c = dict(CONFIGS[cfg_name])
+    c["name"] = cfg_name
+    if a.iters is not None and cfg_name == a.config:
         c["iters"] = a.iters
     dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
     shapes = c["shapes"]
     S = max(1, a.sets)
-
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     sets = [[torch.randn(s, generator=gen, device=dev, dtype=torch.float32).to(dtype) for s in shapes]
             for _ in range(S)]
@@ -240,7 +298,7 @@ def main():
     torch.cuda.synchronize()
 
     # timed regions: K plain steps each (no instrumentation inside); cold = rotating sets
-    do_cold, do_warm = a.mode in ("both", "cold"), a.mode in ("both", "warm")
+    do_cold, do_warm = mode in ("both", "cold"), mode in ("both", "warm")
     cold = timed(lambda k: psgd.aggregate(sets[k % S]), a.steps, world, dev) if do_cold else None
     warm = timed(lambda k: psgd.aggregate(sets[0]), a.steps, world, dev) if do_warm else None
 
@@ -263,26 +321,28 @@ def main():
     if first_cold is None:
         first_cold = first_warm
 
+    multi = world > 1 or dist_path
     s = 2 if dtype == torch.bfloat16 else 4
     grad_bytes = sum(numel(x) for x in shapes) * s
     mask = psgd.is_compressed_mask
     # which final pass each timed step took (I odd: steps alternate between the fused last odd
     # iteration and k_apply); bytes are averaged over the timed steps
-    forms = [codec._plan.fused_final(t, world == 1) for t in range(first_cold, first_cold + a.steps)]
+    forms = [codec._plan.fused_final(t, not multi) for t in range(first_cold, first_cold + a.steps)]
     nf = sum(1 for f in forms if f)
     frac_f = nf / a.steps
-    ab = frac_f * apply_alg_bytes(c, mask, world, True) + (1 - frac_f) * apply_alg_bytes(c, mask, world, False)
-    sb = frac_f * step_alg_bytes(c, mask, world, True) + (1 - frac_f) * step_alg_bytes(c, mask, world, False)
+    wb = 2 if multi else 1  # the byte model of the multi-GPU path (no output in the fused pass)
+    ab = frac_f * apply_alg_bytes(c, mask, wb, True) + (1 - frac_f) * apply_alg_bytes(c, mask, wb, False)
+    sb = frac_f * step_alg_bytes(c, mask, wb, True) + (1 - frac_f) * step_alg_bytes(c, mask, wb, False)
     kf = ("k_final_proj (fused last odd iteration, projection form: G X, residual G - G X X^T, output G X X^T)"
           if nf and all(f == 2 for f in forms if f) else
-          "k_final_odd (fused last odd iteration: product + residual" + (" + output)" if world == 1 else ")"))
+          "k_final_odd (fused last odd iteration: product + residual" + (")" if multi else " + output)"))
     kname = kf if nf == a.steps else "k_apply (fused residual + output)" if nf == 0 else f"{kf} / k_apply, alternating"
 
     def roof(apply_ms, cache, lps):
         ach = ab / (apply_ms * 1e-3) / 1e9
         return {"kernel": kname, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_pmc_traffic(a.config, cache) if world == 1 else None,
+                "traffic": load_pmc_traffic(cfg_name, cache) if not multi else None,
                 "alg_bytes_per_launch": round(ab), "avg_launch_us": round(apply_ms * 1e3, 2),
                 "launches_per_step": round(lps, 2), "cache": cache}
 
@@ -307,13 +367,13 @@ def main():
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
         "data": "synthetic N(0,1) gradients of the named parameter shapes (torch.randn on device), " +
                 (f"{S} independent sets rotated per step (cold Infinity Cache)" if do_cold else "one set (warm)"),
-        "config": {"workload": a.config, "rank": c["rank"], "num_iters_per_step": c["iters"],
+        "config": {"workload": cfg_name, "rank": c["rank"], "num_iters_per_step": c["iters"],
                    "min_compression_rate": c["mcr"], "tensors": len(shapes),
                    "compressed_tensors": sum(mask), "gradient_bytes_per_rank": grad_bytes,
                    "parallelism": f"dp{world}", "cache": "cold" if do_cold else "warm",
                    "gradient_sets": S if do_cold else 1,
                    "buckets": len(codec._buckets) if codec._buckets else 1,
-                   "backend": (backend if world > 1 else None)},
+                   "backend": (backend if multi else None)},
         "per_rank_GBs": round(value / world, 3),
         "roofline": roof(apply_ms_cold, "cold", lps_cold) if do_cold else roof(apply_ms_warm, "warm", lps_warm),
         "step_roofline": step_roof(head),
@@ -322,14 +382,9 @@ def main():
         out["warm"] = {"value": round(world * grad_bytes * a.steps / warm / 1e9, 3),
                        "ms_per_step": round(warm / a.steps * 1e3, 4),
                        "roofline": roof(apply_ms_warm, "warm", lps_warm), "step_roofline": step_roof(warm)}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(c, a.cpu_seconds)
-    elif rank == 0:
-        out["cpu_baseline"] = None
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    del sets, params, psgd
+    torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

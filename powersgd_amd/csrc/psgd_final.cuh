@@ -43,43 +43,6 @@ struct FinNT {
 // slot past the row end or past the matrix gets offset kOob, which loads 0 and drops the
 // store in hardware (no clamping, no branches). The plan keeps a fused matrix below 2^31
 // bytes.
-// Store cache policy of the streaming outputs (residual, output): 2 = nt (gfx950 CPol:
-// sc0 = 1, nt = 2, sc1 = 16), 0 = default. nt keeps the 204 MB a ResNet-50 final pass writes
-// from sitting dirty in the Infinity Cache, where their write-back competed with the NEXT
-// step's cold gradient reads: the even product took 33 us after default-policy stores, 28 us
-// after nt ones (profiles/r02/ab_nt). Build-time knob for A/B runs.
-#ifndef PSGD_ST_AUX
-#define PSGD_ST_AUX 2
-#endif
-
-template <typename T>
-struct FinIo;
-
-template <>
-struct FinIo<float> {
-    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        const v4u x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, PSGD_ST_AUX);
-    }
-    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, PSGD_ST_AUX);
-    }
-};
-
-template <>
-struct FinIo<bf16_t> {
-    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
-        typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
-        const v2u_ x = {uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
-                        uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, PSGD_ST_AUX);
-    }
-    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, PSGD_ST_AUX);
-    }
-};
-
 // Four consecutive row elements [c, c+4) at element offset `e` (= row * m + c): one vector
 // access with the vector layout (m % 4 == 0, aligned), else four scalar accesses.
 template <typename T, bool VEC>
@@ -96,10 +59,10 @@ template <typename T, bool VEC>
 __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c, int32_t m, const float (&v)[4]) {
     constexpr uint32_t s = sizeof(T);
     if constexpr (VEC) {
-        FinIo<T>::st4(rs, ok ? e * s : kOob, v);
+        StIo<T>::st4(rs, ok ? e * s : kOob, v);
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) FinIo<T>::st1(rs, (ok && c + q < m) ? (e + q) * s : kOob, v[q]);
+        for (int q = 0; q < 4; ++q) StIo<T>::st1(rs, (ok && c + q < m) ? (e + q) * s : kOob, v[q]);
     }
 }
 
@@ -462,7 +425,8 @@ template <typename T, int R, int NI, int V>
 __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
-    const gptr<T> O = gmut<T>(a.out) + d.out_off;
+    const rsrc_t rO = make_rsrc(static_cast<T*>(a.out) + d.out_off + g.row_begin * g.m,
+                                uint32_t((g.row_end - g.row_begin) * g.m * int64_t(sizeof(T))));
     const int nt = NI > 0 ? NI : a.nterms;
     constexpr int NC = NI > 0 ? NI : 1;
     float ba[NC][V][R];
@@ -494,7 +458,7 @@ __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& 
                 o[v] = o[v] + alpha * dotr<R>(aa, bb);
             }
         }
-        if (g.active) Io<T>::st(O + int64_t(row) * g.m + g.col0, o);
+        if (g.active) st_vec<T>(rO, uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T)), o);
     }
 }
 

@@ -60,11 +60,54 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 // exec-mask branch and a vmcnt(0) wait per load).
 __device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
 
-// streaming stores (residual, output, flat pack) with the nt cache policy; see PSGD_ST_AUX in
-// psgd_final.cuh for the measurement (build-time knob for A/B runs)
-#ifndef PSGD_NT_STORES
-#define PSGD_NT_STORES 1
+// Streaming outputs (residual, output, flat pack) go through buffer descriptors with an explicit
+// cache policy (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16). Default sc0 | nt | sc1: the
+// 200+ MB a final pass writes must not sit dirty in the Infinity Cache, where the NEXT step's
+// cold gradient reads would pay for their write-back: the following even product ran 30 -> 23.6
+// us, and the rank-4 final pass itself 60 -> 53 us, against nt alone (profiles/r03/st_aux.txt;
+// plain stores were worse still, 33 us). Build-time knob for A/B runs.
+#ifndef PSGD_ST_AUX
+#define PSGD_ST_AUX 19
 #endif
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOob = 0x80000000u;  // beyond every descriptor (num_records < 2^31)
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(bytes), 0x00020000);
+}
+
+template <typename T>
+struct StIo;
+
+template <>
+struct StIo<float> {
+    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, PSGD_ST_AUX);
+    }
+    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, PSGD_ST_AUX);
+    }
+};
+
+template <>
+struct StIo<bf16_t> {
+    static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
+        typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
+        const v2u_ x = {uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
+                        uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, PSGD_ST_AUX);
+    }
+    static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, PSGD_ST_AUX);
+    }
+};
+// V consecutive elements at byte offset `off` of descriptor r
+template <typename T>
+__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[4]) { StIo<T>::st4(r, off, v); }
+template <typename T>
+__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[1]) { StIo<T>::st1(r, off, v[0]); }
 
 template <typename T>
 struct Io;
@@ -76,15 +119,6 @@ struct Io<float> {
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
     }
     static __device__ __forceinline__ void ld(gptr<const float> p, float (&v)[1]) { v[0] = *p; }
-    static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[4]) {
-        const v4f x = {v[0], v[1], v[2], v[3]};
-#if PSGD_NT_STORES
-        __builtin_nontemporal_store(x, (gptr<v4f>)p);
-#else
-        *(gptr<v4f>)p = x;
-#endif
-    }
-    static __device__ __forceinline__ void st(gptr<float> p, const float (&v)[1]) { *p = v[0]; }
 };
 
 template <>
@@ -97,17 +131,6 @@ struct Io<bf16_t> {
         v[3] = __uint_as_float(x.y & 0xffff0000u);
     }
     static __device__ __forceinline__ void ld(gptr<const bf16_t> p, float (&v)[1]) { v[0] = bf2f(*p); }
-    static __device__ __forceinline__ void st(gptr<bf16_t> p, const float (&v)[4]) {
-        v2u x;
-        x.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-        x.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-#if PSGD_NT_STORES
-        __builtin_nontemporal_store(x, (gptr<v2u>)p);
-#else
-        *(gptr<v2u>)p = x;
-#endif
-    }
-    static __device__ __forceinline__ void st(gptr<bf16_t> p, const float (&v)[1]) { *p = f2bf(v[0]); }
 };
 
 // r (<= R) consecutive fp32 factor values, zeros for c >= r. When r == R the row start is
@@ -231,7 +254,10 @@ __device__ __forceinline__ void flat_pack_item(const FlatArgs& a, int item) {
     const FlatItem it = a.items[item];
     const FlatEntry en = a.entries[it.entry];
     const gptr<T> x = gmut<T>(a.tensors[en.tensor]);
-    const gptr<T> f = gmut<T>(a.flat) + en.off;
+    // this item's ranges of the tensor and of the flat buffer (stores past them drop)
+    const uint32_t nb = uint32_t((en.numel - it.start < kFlatItem ? en.numel - it.start : kFlatItem) * sizeof(T));
+    const rsrc_t rx = make_rsrc(static_cast<T*>(a.tensors[en.tensor]) + it.start, nb);
+    const rsrc_t rf = make_rsrc(static_cast<T*>(a.flat) + en.off + it.start, nb);
     const float w = float(a.world);
     float v[PER];
 #pragma unroll
@@ -247,10 +273,9 @@ __device__ __forceinline__ void flat_pack_item(const FlatArgs& a, int item) {
     for (int q = 0; q < PER; ++q) {
         const int64_t j = it.start + int64_t(q) * NT + threadIdx.x;
         if (j < en.numel) {
-            float t[1] = {a.world != 1 ? v[q] / w : v[q]};
-            Io<T>::st(f + j, t);
-            const float z[1] = {0.f};
-            Io<T>::st(x + j, z);
+            const uint32_t off = uint32_t(int64_t(q) * NT + threadIdx.x) * uint32_t(sizeof(T));
+            StIo<T>::st1(rf, off, a.world != 1 ? v[q] / w : v[q]);
+            StIo<T>::st1(rx, off, 0.f);
         }
     }
 }
@@ -588,8 +613,6 @@ constexpr int kOddXT = kOddSW + 4;      // padded row of the transposed X strip 
 // tile's last row): the hardware range check returns 0 for rows past the tile, and a slot
 // whose columns lie past the strip gets offset kOob (also 0, and no memory traffic). Every
 // load is therefore unconditional, unclamped and unmasked.
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr uint32_t kOob = 0x80000000u;  // beyond every descriptor (num_records < 2^31)
 
 template <typename T>
 struct BufIo;
@@ -855,8 +878,13 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
     const gptr<T> G = gmut<T>(a.grads[t.tensor]);
-    const gptr<T> D = a.rdst ? gmut<T>(a.rdst[d.tensor]) : G;  // residual destination
-    const gptr<T> O = a.odst ? gmut<T>(a.odst[d.tensor]) : gmut<T>(a.out) + d.out_off;
+    // residual and output destinations: this tile's rows through buffer descriptors (streaming
+    // cache policy, 32-bit offsets from the tile's first row)
+    T* const Dp = static_cast<T*>(a.rdst ? a.rdst[d.tensor] : a.grads[t.tensor]);
+    T* const Op = a.odst ? static_cast<T*>(a.odst[d.tensor]) : static_cast<T*>(a.out) + d.out_off;
+    const uint32_t tb = uint32_t((g.row_end - g.row_begin) * g.m * int64_t(sizeof(T)));
+    const rsrc_t rD = make_rsrc(Dp + g.row_begin * g.m, tb);
+    const rsrc_t rO = make_rsrc(Op + g.row_begin * g.m, tb);
     const int nt = NI > 0 ? NI : a.nterms;
     constexpr int NC = NI > 0 ? NI : 1;
     constexpr int NA = (NI > 0 && !SHARED) ? NI : 1;
@@ -947,8 +975,9 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
                 }
             }
             if (g.active && row + u * g.stride < g.row_end) {
-                Io<T>::st(D + b.rc[u] * g.m + g.col0, b.x[u]);
-                Io<T>::st(O + b.rc[u] * g.m + g.col0, o);
+                const uint32_t off = uint32_t((b.rc[u] - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
+                st_vec<T>(rD, off, b.x[u]);
+                st_vec<T>(rO, off, o);
             }
         }
     };

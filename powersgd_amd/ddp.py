@@ -61,23 +61,47 @@ class PowerSGDState:
         self._pending: List[tuple] = []
 
     def _arrive(self, bucket: "dist.GradBucket") -> "torch.futures.Future[torch.Tensor]":
-        params, grads = bucket.parameters(), bucket.gradients()
-        idx = []
-        for p, g in zip(params, grads):
-            i = self._index.get(id(p))
-            if i is None:
-                raise RuntimeError("DDP bucket holds a parameter that PowerSGDState was not given")
-            if self._seen[i]:
-                raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
-            self.views[i].add_(g)  # error feedback: residual + fresh gradient
-            self._seen[i] = True
-            self._nseen += 1
-            idx.append(i)
         fut: torch.futures.Future = torch.futures.Future()
-        self._pending.append((bucket.buffer(), grads, idx, fut))
-        if self._nseen == len(self.params):
-            self._complete()
+        try:
+            params, grads = bucket.parameters(), bucket.gradients()
+            idx = []
+            for p, g in zip(params, grads):
+                i = self._index.get(id(p))
+                if i is None:
+                    raise RuntimeError("DDP bucket holds a parameter that PowerSGDState was not given")
+                if self._seen[i]:
+                    raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
+                idx.append(i)
+            for g, i in zip(grads, idx):
+                self.views[i].add_(g)  # error feedback: residual + fresh gradient
+                self._seen[i] = True
+                self._nseen += 1
+            self._pending.append((bucket.buffer(), grads, idx, fut))
+            if self._nseen == len(self.params):
+                self._complete()
+            elif bucket.is_last():
+                # DDP's last bucket arrived but some trainable parameter never did (e.g. one
+                # DDP ignores): no aggregate can run, and waiting would hang DDP's backward
+                missing = [i for i, s in enumerate(self._seen) if not s]
+                raise RuntimeError(f"powersgd_hook: {len(missing)} parameter(s) given to PowerSGDState never "
+                                   f"reached a DDP bucket (first index {missing[0]}); give the state exactly "
+                                   "the parameters DDP reduces")
+        except Exception as e:
+            self._fail(e, fut)
+            raise
         return fut
+
+    def _fail(self, err: Exception, fut: "torch.futures.Future") -> None:
+        """Fail this iteration: every pending bucket future (and this one) gets the exception, so
+        DDP's wait raises instead of hanging, and the next iteration starts clean."""
+        pending, self._pending = self._pending, []
+        self._seen = [False] * len(self.params)
+        self._nseen = 0
+        for *_, f in pending:
+            if not f.done():
+                f.set_exception(err)
+        if not fut.done():
+            fut.set_exception(err)
 
     def _complete(self) -> None:
         outs = self.powersgd.aggregate(self.views)  # leaves the new residual in self.views

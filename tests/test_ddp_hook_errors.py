@@ -1,0 +1,117 @@
+"""CPU tests of the DDP hook's failure paths (powersgd_amd/ddp.py): an iteration that cannot
+aggregate must fail every bucket future it handed to DDP (so DDP's wait raises instead of
+hanging) and leave the state clean for the next iteration. The codec itself is replaced by a
+stub here (the real one needs a GPU); tests/test_gpu_training.py runs the hook end to end."""
+import pytest
+import torch
+
+from powersgd_amd.ddp import PowerSGDState, powersgd_hook
+
+
+class _Bucket:
+    """The GradBucket surface the hook uses."""
+
+    def __init__(self, params, last):
+        self._params = params
+        self._grads = [torch.ones_like(p) for p in params]
+        self._buf = torch.cat([g.view(-1) for g in self._grads])
+        off = 0
+        views = []
+        for g in self._grads:
+            views.append(self._buf[off:off + g.numel()].view(g.shape))
+            off += g.numel()
+        self._grads = views
+        self._last = last
+
+    def parameters(self):
+        return self._params
+
+    def gradients(self):
+        return self._grads
+
+    def buffer(self):
+        return self._buf
+
+    def is_last(self):
+        return self._last
+
+
+class _Codec:
+    def __init__(self, fail=False):
+        self.fail = fail
+
+    def aggregate(self, views):
+        if self.fail:
+            raise RuntimeError("collective failed")
+        return [v.clone() for v in views]
+
+
+def _state(params, codec):
+    st = object.__new__(PowerSGDState)  # the constructor builds a GPU codec: bypass it
+    st.params = params
+    st._index = {id(p): i for i, p in enumerate(params)}
+    st.residual = torch.zeros(sum(p.numel() for p in params))
+    st.views, off = [], 0
+    for p in params:
+        st.views.append(st.residual[off:off + p.numel()].view(p.shape))
+        off += p.numel()
+    st.powersgd = codec
+    st._seen = [False] * len(params)
+    st._nseen = 0
+    st._pending = []
+    return st
+
+
+def _params(n=3):
+    return [torch.nn.Parameter(torch.zeros(4, 2)) for _ in range(n)]
+
+
+def test_complete_iteration_sets_every_future():
+    ps = _params()
+    st = _state(ps, _Codec())
+    f1 = powersgd_hook(st, _Bucket(ps[:2], False))
+    assert not f1.done()
+    f2 = powersgd_hook(st, _Bucket(ps[2:], True))
+    assert f1.done() and f2.done()
+    assert torch.equal(f1.value(), torch.ones(16)) and torch.equal(f2.value(), torch.ones(8))
+    assert st._nseen == 0 and st._pending == []
+
+
+def test_failed_aggregate_fails_pending_futures_and_resets():
+    ps = _params()
+    st = _state(ps, _Codec(fail=True))
+    f1 = powersgd_hook(st, _Bucket(ps[:2], False))
+    with pytest.raises(RuntimeError, match="collective failed"):
+        powersgd_hook(st, _Bucket(ps[2:], True))
+    assert f1.done()
+    with pytest.raises(RuntimeError, match="collective failed"):
+        f1.wait()
+    assert st._nseen == 0 and st._pending == [] and not any(st._seen)
+    st.powersgd = _Codec()  # the next iteration starts clean
+    powersgd_hook(st, _Bucket(ps[:2], False))
+    f = powersgd_hook(st, _Bucket(ps[2:], True))
+    assert f.done()
+
+
+def test_parameter_ddp_never_buckets_raises_instead_of_hanging():
+    ps = _params()
+    st = _state(ps, _Codec())
+    f1 = powersgd_hook(st, _Bucket(ps[:1], False))
+    with pytest.raises(RuntimeError, match="never reached a DDP bucket"):
+        powersgd_hook(st, _Bucket(ps[1:2], True))  # ps[2] never arrives
+    with pytest.raises(RuntimeError):
+        f1.wait()
+    assert st._nseen == 0 and st._pending == []
+
+
+def test_unknown_parameter_and_double_arrival():
+    ps = _params()
+    st = _state(ps, _Codec())
+    with pytest.raises(RuntimeError, match="was not given"):
+        powersgd_hook(st, _Bucket([torch.nn.Parameter(torch.zeros(2))], False))
+    f1 = powersgd_hook(st, _Bucket(ps[:1], False))
+    with pytest.raises(RuntimeError, match="twice"):
+        powersgd_hook(st, _Bucket(ps[:1], False))
+    with pytest.raises(RuntimeError):
+        f1.wait()
+    assert st._nseen == 0

@@ -1,14 +1,15 @@
 """Kernel sequence of the last steps of a rocprofv3 kernel trace: per dispatch its start
 offset from the first shown dispatch, duration and the gap since the previous one (us).
-usage: python tools/kt_seq.py <dir> [ndispatches]"""
+usage: python tools/kt_seq.py <dir> [ndispatches] [all]"""
 import csv
 import glob
 import sys
 
 rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + '/**/*kernel_trace.csv', recursive=True)[0])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-rows = [r for r in rows if 'psgd' in r['Kernel_Name'] or 'rocclr' in r['Kernel_Name']]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+if not (len(sys.argv) > 3 and sys.argv[3] == "all"):  # "all": RCCL and torch kernels too
+    rows = [r for r in rows if 'psgd' in r['Kernel_Name'] or 'rocclr' in r['Kernel_Name']]
 rows = rows[-n:]
 t0 = int(rows[0]['Start_Timestamp'])
 prev = None

@@ -12,13 +12,13 @@ for spec in $@; do
     (
       export PSGD_LIB_PATH=$PWD/$lib
       for e in ${envs//,/ }; do export $e; done
-      timeout -k 10 120 python3 bench.py --config $cfg --steps 40 --warmup 10 --mode cold --no-cpu-baseline > "$out/$tag.json" 2> "$out/$tag.err" || exit 1
-      timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$out/kt_$tag" -o kt -- python3 bench.py --config $cfg --steps 20 --warmup 4 --mode cold --no-cpu-baseline > /dev/null 2>&1 || exit 1
+      timeout -k 10 120 python3 bench.py --config $cfg --steps 40 --warmup 10 --mode cold --no-cpu-baseline --no-extra > "$out/$tag.json" 2> "$out/$tag.err" || exit 1
+      timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "/tmp/kt_$tag" -o kt -- python3 bench.py --config $cfg --steps 20 --warmup 4 --mode cold --no-cpu-baseline --no-extra > /dev/null 2>&1 || exit 1
     ) || exit 1
     python3 - "$out" "$tag" <<'PY'
 import csv, glob, json, statistics, sys
 out, tag = sys.argv[1], sys.argv[2]
-rows = list(csv.DictReader(open(glob.glob(f"{out}/kt_{tag}/**/*kernel_trace.csv", recursive=True)[0])))
+rows = list(csv.DictReader(open(glob.glob(f"/tmp/kt_{tag}/**/*kernel_trace.csv", recursive=True)[0])))
 def avg(name):
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if name in r["Kernel_Name"]]
     return statistics.median(d[-16:]) if d else float("nan")
