@@ -186,6 +186,11 @@ def main():
     env_world = os.environ.get("WORLD_SIZE")
     if a.gpus > 1 and env_world is None:
         sys.exit(launch_ranks(a))
+    # stdout carries exactly ONE JSON line: anything else printed at the C level (RCCL's
+    # version banner at communicator init) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -198,7 +203,7 @@ def main():
             torch.distributed.init_process_group(backend)
             world = torch.distributed.get_world_size()
         if rank == 0:
-            print(json.dumps({"n_gpus": world, "backend": backend if world > 1 else None}), flush=True)
+            os.write(json_fd, (json.dumps({"n_gpus": world, "backend": backend if world > 1 else None}) + "\n").encode())
         if world > 1:
             torch.distributed.destroy_process_group()
         return
@@ -240,7 +245,8 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         torch.distributed.destroy_process_group()
 

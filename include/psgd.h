@@ -48,6 +48,7 @@ extern "C" {
 
 typedef struct psgd_plan psgd_plan;
 typedef struct psgd_flat psgd_flat;
+typedef struct psgd_comm psgd_comm;
 
 enum psgd_status {
     PSGD_OK = 0,
@@ -203,6 +204,27 @@ int psgd_orthogonalize(psgd_plan* plan, int32_t which, float* buf, int32_t mode,
 int psgd_reconstruct(psgd_plan* plan, void* const* grads, void* const* resid_out, void* const* out,
                      int32_t nterms, const float* const* term_p, const float* const* term_q,
                      const float* const* avg_p, const float* const* avg_q, float alpha, void* stream);
+
+/* ------------------------------------ multi-GPU step with RCCL on the caller's stream ------ */
+/* One process per GPU (reference: torch.distributed default group, powersgd.py:204-209 and
+ * utils.py:43-49). The library drives RCCL itself, on the same stream as its kernels, so a
+ * whole world-size-W step is ONE call with no host synchronisation and no per-collective
+ * round trip through the host language. RCCL is resolved at run time (dlopen; an already loaded
+ * librccl, e.g. PyTorch's, is reused): no link-time dependency.
+ *   psgd_comm_unique_id  on rank 0: the communicator id (psgd_comm_id_bytes bytes), which the
+ *                        caller broadcasts to every rank (e.g. torch.distributed);
+ *   psgd_comm_init       on every rank, collectively: a communicator of `world` ranks on `device`.
+ * psgd_aggregate_comm: PowerSGD.aggregate at world size W (reference :64-74 with
+ * is_distributed()): for every power iteration the codec kernels and an in-place SUM all-reduce
+ * of the out-factor state buffer (:204-209; the last iteration's collective grouped with the
+ * SUM all-reduce of the uncompressed tensors packed /W into flat_out, utils.py:43-47), then the
+ * output pass (alpha = 1/W). flat may be null (no uncompressed tensors). */
+int psgd_comm_id_bytes(int64_t* bytes);
+int psgd_comm_unique_id(void* id_out);
+int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, psgd_comm** out);
+int psgd_comm_destroy(psgd_comm* comm);
+int psgd_aggregate_comm(psgd_plan* plan, void* const* grads, void* out, int64_t step, psgd_flat* flat,
+                        void* const* unc, void* flat_out, psgd_comm* comm, void* stream);
 
 /* ------------------------------------------ uncompressed tensors: flat average ------ */
 /* AllReduce.aggregate minus the collective: flat[off_i + e] = x_i[e] / world_size (exact

@@ -53,6 +53,11 @@ _SIGNATURES = {
     "psgd_plan_bucket_range": ([_vp, _i32, _P_i64, _P_i64, _P_i64, _P_i64], _i32),
     "psgd_compress_bucket": ([_vp, _vp, _i64, _i32, _i32, _vp], _i32),
     "psgd_decompress_bucket": ([_vp, _vp, _vp, _i64, _i32, _i32, _vp], _i32),
+    "psgd_comm_id_bytes": ([_P_i64], _i32),
+    "psgd_comm_unique_id": ([_vp], _i32),
+    "psgd_comm_init": ([_i32, _i32, _vp, _i32, ctypes.POINTER(_vp)], _i32),
+    "psgd_comm_destroy": ([_vp], _i32),
+    "psgd_aggregate_comm": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp], _i32),
     "psgd_ipc_handle_bytes": ([_P_i64], _i32),
     "psgd_ipc_create": ([_vp, _vp], _i32),
     "psgd_ipc_open": ([_vp, _i32, _i32, _vp], _i32),
@@ -199,6 +204,11 @@ class Plan:
                                            ctypes.byref(ql)))
         return po.value, pl.value, qo.value, ql.value
 
+    def aggregate_comm(self, grads, out_ptr: int, step: int, flat, unc, flat_out: int, comm: "Comm",
+                       stream: int) -> None:
+        check(lib().psgd_aggregate_comm(self._h, grads, out_ptr, step, flat._h if flat else None, unc, flat_out,
+                                        comm._h, stream))
+
     def compress_bucket(self, grads, step: int, it: int, bucket: int, stream: int) -> None:
         check(lib().psgd_compress_bucket(self._h, grads, step, it, bucket, stream))
 
@@ -282,6 +292,32 @@ class FlatPlan:
 
     def pack(self, tensors, flat_ptr: int, world: int, stream: int) -> None:
         check(lib().psgd_flat_pack(self._h, tensors, flat_ptr, world, stream))
+
+
+def comm_unique_id() -> bytes:
+    """RCCL communicator id (rank 0); the caller broadcasts it to every rank."""
+    n = _i64()
+    check(lib().psgd_comm_id_bytes(ctypes.byref(n)))
+    buf = (ctypes.c_uint8 * n.value)()
+    check(lib().psgd_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """Owns a psgd_comm: an RCCL communicator the library drives on the codec's stream."""
+
+    def __init__(self, world: int, rank: int, uid: bytes, device: int):
+        arr = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid)
+        h = _vp()
+        check(lib().psgd_comm_init(world, rank, arr, device, ctypes.byref(h)))
+        self._h = h
+        self.world = world
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.psgd_comm_destroy(h)
+            self._h = None
 
 
 def should_compress(shape: Sequence[int], rank: int, iters: int, min_rate: float) -> bool:

@@ -1,0 +1,146 @@
+// RCCL inside libpsgd: communicators and the stream-ordered SUM all-reduce of a world-size-W
+// step (psgd_aggregate_comm, psgd_plan.cpp). RCCL is resolved at run time with dlopen/dlsym
+// (psgd_comm_* in include/psgd.h): an RCCL the process has already loaded (PyTorch's) is reused,
+// else PSGD_RCCL_LIB or the ROCm one; the library has no link-time dependency on it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "psgd.h"
+#include "psgd_internal.h"
+
+struct psgd_comm {
+    ncclComm_t comm = nullptr;
+    int world = 0, rank = -1, device = -1;
+};
+
+namespace psgd {
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string error;
+};
+
+Rccl load() {
+    Rccl r;
+    void* h = nullptr;
+    // 1. an RCCL already in the process (the host framework's), 2. PSGD_RCCL_LIB, 3. ROCm's
+    for (const char* name : {"librccl.so", "librccl.so.1"}) {
+        if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    }
+    const char* env = std::getenv("PSGD_RCCL_LIB");
+    if (!h && env && *env) h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        r.error = std::string("cannot load librccl.so: ") + (dlerror() ? dlerror() : "?");
+        return r;
+    }
+    auto sym = [&](const char* n) { return dlsym(h, n); };
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+    r.init_rank = reinterpret_cast<decltype(r.init_rank)>(sym("ncclCommInitRank"));
+    r.destroy = reinterpret_cast<decltype(r.destroy)>(sym("ncclCommDestroy"));
+    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(sym("ncclAllReduce"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+    if (!r.get_unique_id || !r.init_rank || !r.destroy || !r.all_reduce || !r.group_start || !r.group_end ||
+        !r.error_string)
+        r.error = "librccl.so lacks an expected symbol";
+    return r;
+}
+
+const Rccl& rccl() {
+    static const Rccl r = load();
+    return r;
+}
+
+int rccl_fail(ncclResult_t e, const char* what) {
+    const Rccl& r = rccl();
+    return comm_fail(PSGD_ERR_DEVICE, (std::string(what) + ": " + (r.error_string ? r.error_string(e) : "?")).c_str());
+}
+
+}  // namespace
+
+int comm_world(const psgd_comm* c) { return c->world; }
+
+int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s) {
+    const Rccl& r = rccl();
+    if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
+    ncclResult_t e = r.group_start();
+    if (e != ncclSuccess) return rccl_fail(e, "ncclGroupStart");
+    if (n) e = r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, s);
+    if (e == ncclSuccess && n2) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
+    const ncclResult_t e2 = r.group_end();
+    if (e != ncclSuccess) return rccl_fail(e, "ncclAllReduce");
+    if (e2 != ncclSuccess) return rccl_fail(e2, "ncclGroupEnd");
+    return PSGD_OK;
+}
+
+}  // namespace psgd
+
+using namespace psgd;
+
+extern "C" {
+
+int psgd_comm_id_bytes(int64_t* bytes) {
+    if (!bytes) return comm_fail(PSGD_ERR_VALUE, "null argument");
+    *bytes = int64_t(sizeof(ncclUniqueId));
+    return PSGD_OK;
+}
+
+int psgd_comm_unique_id(void* id_out) {
+    if (!id_out) return comm_fail(PSGD_ERR_VALUE, "null argument");
+    const Rccl& r = rccl();
+    if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
+    ncclUniqueId id;
+    const ncclResult_t e = r.get_unique_id(&id);
+    if (e != ncclSuccess) return rccl_fail(e, "ncclGetUniqueId");
+    std::memcpy(id_out, &id, sizeof(id));
+    return PSGD_OK;
+}
+
+int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, psgd_comm** out) {
+    if (!id || !out) return comm_fail(PSGD_ERR_VALUE, "null argument");
+    *out = nullptr;
+    if (world < 1 || rank < 0 || rank >= world) return comm_fail(PSGD_ERR_VALUE, "bad world/rank");
+    const Rccl& r = rccl();
+    if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (device >= 0) (void)hipSetDevice(device);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    auto* c = new psgd_comm();
+    const ncclResult_t e = r.init_rank(&c->comm, world, uid, rank);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    if (e != ncclSuccess) {
+        delete c;
+        return rccl_fail(e, "ncclCommInitRank");
+    }
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    *out = c;
+    return PSGD_OK;
+}
+
+int psgd_comm_destroy(psgd_comm* c) {
+    if (!c) return PSGD_OK;
+    if (c->comm) (void)rccl().destroy(c->comm);
+    delete c;
+    return PSGD_OK;
+}
+
+}  // extern "C"

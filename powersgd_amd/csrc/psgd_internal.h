@@ -4,7 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct psgd_comm;  // include/psgd.h (psgd_comm.cpp)
+
 namespace psgd {
+
+// host side of the RCCL communicator (psgd_comm.cpp): the error message goes to
+// psgd_last_error (comm_fail, psgd_plan.cpp); comm_allreduce = a grouped in-place SUM of one or
+// two fp32 buffers, stream-ordered on s
+int comm_fail(int code, const char* msg);
+int comm_world(const psgd_comm* c);
+int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
 
 constexpr int kMaxTerms = 16;   // == PSGD_MAX_ITERS
 constexpr int kBlock = 256;     // threads per workgroup for the streaming kernels

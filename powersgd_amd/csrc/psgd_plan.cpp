@@ -299,6 +299,10 @@ struct DevScope {  // make `dev` current for the scope, restore afterwards
 
 }  // namespace
 
+namespace psgd {
+int comm_fail(int code, const char* msg) { return fail(code, msg); }
+}  // namespace psgd
+
 // Persistent even product (k_even): workgroups per launch (CUs x workgroups per CU), at least
 // kEvenMinElems gradient elements per workgroup (small plans use fewer, fuller workgroups), at
 // most kMaxBuckets buckets (each bucket launch spreads over the whole chip).
@@ -1958,6 +1962,40 @@ int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t ste
     FlatArgs a;
     if (int st = flat_args(f, unc, flat_out, 1, s, &a)) return st;
     return aggregate_entry(p, grads, out, step, s, &a, f);
+}
+
+// World size W in one call (include/psgd.h): per iteration the kernels, then the in-place SUM
+// all-reduce of the out-factor state on the same stream (the last grouped with the flat
+// buffer of the uncompressed tensors), then the output pass. Same sequence as the building
+// blocks psgd_compress / all_reduce / psgd_decompress (reference powersgd.py:172-230).
+int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f, void* const* unc,
+                        void* flat_out, psgd_comm* comm, void* stream) {
+    if (!p || !grads || !out || !comm) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (p->f64()) return fail(PSGD_ERR_DTYPE, "psgd_aggregate_comm takes fp32/bf16 plans (fp32 factors)");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    const bool has_flat = f && f->total > 0;
+    if (has_flat) {
+        if (!unc || !flat_out) return fail(PSGD_ERR_VALUE, "null argument");
+        if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
+        if (f->dtype != PSGD_F32) return fail(PSGD_ERR_DTYPE, "psgd_aggregate_comm packs fp32 uncompressed tensors");
+    }
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int world = comm_world(comm);
+    if (has_flat)  // x / W into the flat buffer, x = 0 (utils.py:43-47, powersgd.py:29-30)
+        if (int st = psgd_flat_pack(f, unc, flat_out, world, stream)) return st;
+    for (int it = 0; it < p->iters; ++it) {
+        if (int st = compress_impl(p, grads, step, it, s, false, false)) return st;
+        const bool e = p->even(step, it);
+        const bool last = it == p->iters - 1;
+        if (int st = comm_allreduce(comm, e ? p->Q : p->P, size_t(e ? p->qtot : p->ptot),
+                                    last && has_flat ? static_cast<float*>(flat_out) : nullptr,
+                                    last && has_flat ? size_t(f->total) : 0, s))
+            return st;
+    }
+    return decompress_impl(p, grads, out, step, world, s, false);
 }
 
 }  // extern "C"

@@ -177,7 +177,20 @@ class PowerSGD(Aggregator):
         if not isinstance(gradients, list):
             gradients = list(gradients)
         self._table.fill(gradients)  # reference _split :76-84 + the checks its torch ops make
-        if self._unc is not None and is_distributed() and self._merge_ok:
+        comm = self._powersgd._rccl_comm() if is_distributed() else None
+        if comm is not None:
+            # world size W, RCCL: the whole step in one library call on the codec's stream; the
+            # uncompressed tensors (fp32) ride in the last factor collective
+            codec, u = self._powersgd, self._unc
+            if u is not None and u.dtype == torch.float32:
+                unc = u.slab.get()
+                outs = codec._aggregate_table(self._table.comp_addr(),
+                                              flat=(u.plan, self._table.unc_addr(), u.slab.data_ptr())) + unc
+            else:
+                outs = codec._aggregate_table(self._table.comp_addr())
+                if u is not None:
+                    outs = outs + u.run(self._table.unc_addr())
+        elif self._unc is not None and is_distributed() and self._merge_ok:
             outs = self._aggregate_merged()
         elif self._unc is not None and not is_distributed():
             # world size 1: the uncompressed copy/zero rides in the codec's final launch
@@ -281,6 +294,7 @@ class BasicPowerSGD(Aggregator):
         self._q_comm: Optional[torch.Tensor] = None
         self._buckets: Optional[List[tuple]] = None  # W > 1: (p_off, p_len, q_off, q_len) per bucket
         self._ipc_open = False  # W > 1 with PSGD_IPC_ALLREDUCE=1: peers' exchange buffers mapped
+        self._comm = None  # W > 1 over RCCL: the library's own communicator (_rccl_comm)
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
         """reference :146-235. Mutates ``gradients`` into the compression error."""
@@ -288,6 +302,22 @@ class BasicPowerSGD(Aggregator):
             gradients = list(gradients)
         self._table.fill(gradients)  # dtype / device / shape / contiguity checks + pointers
         return self._aggregate_table(self._table.comp_addr())
+
+    def _rccl_comm(self) -> Optional["_lib.Comm"]:
+        """World size > 1 on the NCCL (RCCL) backend: a communicator the library drives itself on
+        the codec's stream (psgd_comm_init; the id travels over the default process group), so a
+        whole step is one call (psgd_aggregate_comm). None on gloo, for fp64 plans, with
+        PSGD_COMM=torch (the torch.distributed path below) or PSGD_IPC_ALLREDUCE=1."""
+        if self._comm is None:
+            self._comm = False
+            dist = torch.distributed
+            if (os.environ.get("PSGD_COMM", "rccl") == "rccl" and dist.get_backend() == "nccl"
+                    and self.dtype != torch.float64 and os.environ.get("PSGD_IPC_ALLREDUCE") != "1"):
+                world, rank = dist.get_world_size(), dist.get_rank()
+                obj = [_lib.comm_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                self._comm = _lib.Comm(world, rank, obj[0], self._dev_index)
+        return self._comm or None
 
     def _attach_tail(self, numel: int) -> None:
         """Re-home the P and Q state buffers at the head of [factor | tail] allocations so
@@ -320,7 +350,11 @@ class BasicPowerSGD(Aggregator):
         out_ptr = self._slab.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
-        if is_distributed():
+        comm = self._rccl_comm() if is_distributed() and last_comm is None else None
+        if comm is not None:
+            f = flat if flat is not None else (None, None, 0)
+            self._plan.aggregate_comm(ptrs, out_ptr, step, f[0], f[1], f[2], comm, stream)
+        elif is_distributed():
             world = torch.distributed.get_world_size()
             iters = self.config.num_iters_per_step
             if os.environ.get("PSGD_IPC_ALLREDUCE") == "1" and last_comm is None and self.dtype != torch.float64:
