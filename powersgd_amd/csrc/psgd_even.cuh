@@ -379,6 +379,10 @@ __global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe
     // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees vec == 0)
     __shared__ __attribute__((aligned(16))) float red[kEvenNW * 64 * (R <= 8 ? 4 : 1) * R];
     __shared__ float ssl[kEvenNW];
+    if (int(blockIdx.x) >= a.nwg) {  // uncompressed tensors (reference utils.py:43-47)
+        flat_pack_item<T, kEvenNT>(a.flat, int(blockIdx.x) - a.nwg);
+        return;
+    }
     const int s0 = a.wg_seg[blockIdx.x], s1 = a.wg_seg[blockIdx.x + 1];
     if (s0 >= s1) return;
     // the next segment's descriptor and gradient pointer are loaded while this one streams
@@ -406,7 +410,8 @@ __global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe
 }
 
 template <typename T, int R>
-hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg, hipStream_t s) {
+hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg0, hipStream_t s) {
+    const int nwg = nwg0 + a.flat.nitems;
     // register-cached error-feedback terms: up to 3 at ranks <= 4, 1 at rank 8 (more spill at
     // the 256-VGPR cap of a 512-thread workgroup)
     constexpr bool kCache = R <= 8;
@@ -432,7 +437,7 @@ hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg, hipStream_t 
 
 template <typename T>
 hipError_t dispatch_even(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s) {
-    if (nwg <= 0) return hipSuccess;
+    if (nwg + a.flat.nitems <= 0) return hipSuccess;
     switch (R) {
         case 1: return dispatch_even_r<T, 1>(nres, a, nwg, s);
         case 2: return dispatch_even_r<T, 2>(nres, a, nwg, s);

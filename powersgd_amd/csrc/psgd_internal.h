@@ -140,9 +140,12 @@ struct ProductArgs {
     // segments write sum_rows P^2 of their rows to ss0[seg.ss]
     float* ss0;
     // even product (k_even): segments and per-workgroup [begin, end) (wg_seg[blockIdx],
-    // wg_seg[blockIdx + 1])
+    // wg_seg[blockIdx + 1]) of its nwg workgroups; workgroups nwg .. nwg + flat.nitems - 1 pack
+    // the uncompressed tensors (world size > 1: the first iteration's launch carries them)
     const Seg* segs;
     const int32_t* wg_seg;
+    int32_t nwg;
+    FlatArgs flat;
 };
 
 struct ApplyArgs {

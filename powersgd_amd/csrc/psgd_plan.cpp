@@ -1439,7 +1439,11 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         // persistent k_even: this span's workgroups [wg[0], wg[1]) of the segmentation
         pa.segs = p->dev<Seg>(p->o_segs);
         pa.wg_seg = p->dev<int32_t>(p->o_wg_seg) + sp.wg[0];
-        PSGD_HIP(launch_even(p->dtype, p->rbucket, it, pa, sp.wg[1] - sp.wg[0], s));
+        pa.nwg = sp.wg[1] - sp.wg[0];
+        // world size > 1 (no output written here): the first iteration's launch also packs the
+        // uncompressed tensors, ahead of every collective
+        if (fl && !write_out && it == 0) pa.flat = *fl;
+        PSGD_HIP(launch_even(p->dtype, p->rbucket, it, pa, pa.nwg, s));
     } else {
         if (sp.ov[1] > sp.ov[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov) + sp.ov[0];
@@ -1711,7 +1715,8 @@ int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, 
     if (!odd) {
         pa.segs = p->dev<Seg>(p->o_segs);
         pa.wg_seg = p->dev<int32_t>(p->o_wg_seg);
-        PSGD_HIP(launch_even(p->dtype, p->rbucket, nterms, pa, int(p->wg_seg.size()) - 1, s));
+        pa.nwg = int(p->wg_seg.size()) - 1;
+        PSGD_HIP(launch_even(p->dtype, p->rbucket, nterms, pa, pa.nwg, s));
     } else {
         if (!p->tiles_ov.empty()) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov);
@@ -1984,10 +1989,17 @@ int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t ste
     DevScope scope(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int world = comm_world(comm);
-    if (has_flat)  // x / W into the flat buffer, x = 0 (utils.py:43-47, powersgd.py:29-30)
+    // x / W into the flat buffer, x = 0 (utils.py:43-47, powersgd.py:29-30): inside the first
+    // even product's launch when the step starts even, else its own launch
+    FlatArgs fa{};
+    const bool fold = has_flat && p->even(step, 0);
+    if (fold) {
+        if (int st = flat_args(f, unc, flat_out, world, s, &fa)) return st;
+    } else if (has_flat) {
         if (int st = psgd_flat_pack(f, unc, flat_out, world, stream)) return st;
+    }
     for (int it = 0; it < p->iters; ++it) {
-        if (int st = compress_impl(p, grads, step, it, s, false, false)) return st;
+        if (int st = compress_impl(p, grads, step, it, s, false, false, fold ? &fa : nullptr)) return st;
         const bool e = p->even(step, it);
         const bool last = it == p->iters - 1;
         if (int st = comm_allreduce(comm, e ? p->Q : p->P, size_t(e ? p->qtot : p->ptot),
