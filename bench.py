@@ -225,6 +225,10 @@ def main():
             sys.exit(3)
     dev = torch.device("cuda", local)
     out = measure(a, a.config, world, rank, dev, backend, a.mode)
+    if world > 1 and os.environ.get("PSGD_BENCH_IPC", "1") == "1" and "PSGD_COMM" not in os.environ:
+        # the same step with every factor all-reduce as a one-shot sum over IPC exchange buffers
+        # (device-side flags, no collective library): beside the RCCL headline, not instead of it
+        out["ipc_exchange"] = ipc_block(a, world, rank, dev, backend)
     if rank == 0 and world == 1 and not a.no_extra:
         # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
         # world size 1, cold, same steps
@@ -257,6 +261,19 @@ def CONFIGS_():
     return CONFIGS
 
 
+def ipc_block(a, world, rank, dev, backend):
+    os.environ["PSGD_COMM"] = "ipc"
+    try:
+        m = measure(a, a.config, world, rank, dev, backend, "cold", dist_path=True)
+        blk = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
+        blk["timed_out"] = m.get("ipc_timed_out")
+        return blk
+    except RuntimeError as e:  # setup failures are collective (BasicPowerSGD._ipc_setup)
+        return {"error": str(e)[:300]}
+    finally:
+        del os.environ["PSGD_COMM"]
+
+
 def one_rank_group(a, dev):
     """cfg3 and cfg2 through PowerSGD.aggregate with torch.distributed initialised as ONE RCCL
     rank on this GPU: is_distributed() is True, so the exact multi-GPU code path runs."""
@@ -274,6 +291,17 @@ def one_rank_group(a, dev):
             m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
             res[cfg] = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
             res[cfg]["buckets"] = m["config"]["buckets"]
+        # the IPC exchange path (psgd_aggregate_ipc) of the same configs: its flag handshake and
+        # rank-order sums with W = 1 (own buffer only)
+        os.environ["PSGD_COMM"] = "ipc"
+        try:
+            res["ipc_exchange"] = {}
+            for cfg in ("cfg3_resnet50_r4", "cfg2_resnet50_r1"):
+                m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
+                res["ipc_exchange"][cfg] = {"ms_per_step": m["ms_per_step"], "value": m["value"],
+                                            "timed_out": m.get("ipc_timed_out")}
+        finally:
+            del os.environ["PSGD_COMM"]
         return res
     finally:
         torch.distributed.destroy_process_group()
@@ -384,6 +412,9 @@ def measure(a, cfg_name, world, rank, dev, backend, mode, dist_path=False):
         "roofline": roof(apply_ms_cold, "cold", lps_cold) if do_cold else roof(apply_ms_warm, "warm", lps_warm),
         "step_roofline": step_roof(head),
     }
+    if codec._ipc_open:
+        out["ipc_timed_out"] = codec.ipc_status()
+        codec.close_ipc()
     if do_cold and do_warm:
         out["warm"] = {"value": round(world * grad_bytes * a.steps / warm / 1e9, 3),
                        "ms_per_step": round(warm / a.steps * 1e3, 4),

@@ -18,6 +18,8 @@
  *   psgd_flat_*            AllReduce.aggregate          powersgd/powersgd.py:22-31,
  *                          pack / allreduce_average      powersgd/utils.py:6-10, :43-49
  *   psgd_aggregate_flat    PowerSGD.aggregate           powersgd/powersgd.py:64-74 (world size 1)
+ *   psgd_aggregate_comm    PowerSGD.aggregate at world size W over RCCL (:64-74, :204-209)
+ *   psgd_aggregate_ipc     the same over IPC exchange buffers with device-side flags (one node)
  *
  * Conventions
  *  - No torch types. Device buffers are plain pointers on the plan's device; `stream` is a
@@ -149,19 +151,32 @@ int psgd_compress_bucket(psgd_plan* plan, void* const* grads, int64_t step, int3
 int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64_t step,
                            int32_t world_size, int32_t bucket, void* stream);
 
-/* ----------------------------- one-shot all-reduce of the last factor over IPC (W > 1) ------ */
-/* Single node, one process per GPU: instead of a ring all-reduce of the last iteration's
- * out-factor (powersgd.py:204-209), every rank reads all ranks' copies directly through IPC
- * mappings over xGMI and sums them in rank order. psgd_ipc_create allocates this rank's exchange
- * buffer and exports its handle (psgd_ipc_handle_bytes bytes); the caller all-gathers the handles
- * and calls psgd_ipc_open. Per step, after the last psgd_compress: psgd_ipc_publish (local factor
- * -> exchange buffer), a cross-rank barrier (every rank published; and, before publishing, every
- * rank finished the previous step's sum), psgd_ipc_sum (state <- SUM), then psgd_decompress. */
+/* ------------------------- one-shot all-reduce over IPC, stream-ordered (W > 1, one node) ------ */
+/* PowerSGD.aggregate at world size W (reference powersgd.py:64-74 with is_distributed(); the
+ * factor all-reduce :204-209 and the uncompressed tensors' allreduce_average, utils.py:43-49)
+ * without a collective library: one process per GPU, every rank reads all ranks' local factors
+ * directly through IPC mappings (xGMI between GPUs) and sums them in rank order, so every rank
+ * holds bitwise the same sum. Synchronisation is device-side: per iteration a kernel raises this
+ * rank's epoch flag in its exchange buffer and polls the peers' flags (system scope, bounded: a
+ * peer that never arrives sets the status word read by psgd_ipc_status instead of hanging).
+ * No host barrier and no host synchronisation per step.
+ *   psgd_ipc_create   allocates this rank's exchange buffer (flags + two parities x iterations
+ *                     slots, room for flat_numel uncompressed values) and exports its handle
+ *                     (psgd_ipc_handle_bytes bytes). Synchronous.
+ *   psgd_ipc_open     the caller all-gathers the W handles (e.g. torch.distributed) and passes
+ *                     them in rank order; opens the peers' buffers.
+ *   psgd_aggregate_ipc the whole step on `stream` (same arguments as psgd_aggregate_comm).
+ *   psgd_ipc_status   synchronous: 1 if a wait timed out since the last call (results invalid).
+ *   psgd_ipc_close    synchronous: unmap the peers. Teardown is collective: every rank calls it,
+ *                     then the caller runs a cross-rank barrier before any plan is destroyed
+ *                     (psgd_plan_destroy frees the exchange buffer the peers may still map). */
 int psgd_ipc_handle_bytes(int64_t* bytes);
-int psgd_ipc_create(psgd_plan* plan, void* handle_out);
+int psgd_ipc_create(psgd_plan* plan, int64_t flat_numel, void* handle_out);
 int psgd_ipc_open(psgd_plan* plan, int32_t world_size, int32_t rank, const void* handles);
-int psgd_ipc_publish(psgd_plan* plan, int64_t step, void* stream);
-int psgd_ipc_sum(psgd_plan* plan, int64_t step, void* stream);
+int psgd_aggregate_ipc(psgd_plan* plan, void* const* grads, void* out, int64_t step, psgd_flat* flat,
+                       void* const* unc, void* flat_out, void* stream);
+int psgd_ipc_status(psgd_plan* plan, int32_t* timed_out);
+int psgd_ipc_close(psgd_plan* plan);
 
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);

@@ -59,10 +59,11 @@ _SIGNATURES = {
     "psgd_comm_destroy": ([_vp], _i32),
     "psgd_aggregate_comm": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp], _i32),
     "psgd_ipc_handle_bytes": ([_P_i64], _i32),
-    "psgd_ipc_create": ([_vp, _vp], _i32),
+    "psgd_ipc_create": ([_vp, _i64, _vp], _i32),
     "psgd_ipc_open": ([_vp, _i32, _i32, _vp], _i32),
-    "psgd_ipc_publish": ([_vp, _i64, _vp], _i32),
-    "psgd_ipc_sum": ([_vp, _i64, _vp], _i32),
+    "psgd_aggregate_ipc": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _i32),
+    "psgd_ipc_status": ([_vp, _P_i32], _i32),
+    "psgd_ipc_close": ([_vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -215,12 +216,12 @@ class Plan:
     def decompress_bucket(self, grads, out_ptr: int, step: int, world: int, bucket: int, stream: int) -> None:
         check(lib().psgd_decompress_bucket(self._h, grads, out_ptr, step, world, bucket, stream))
 
-    # --- one-shot all-reduce of the last factor over IPC mappings (W > 1, one node)
-    def ipc_create(self) -> bytes:
+    # --- one-shot all-reduce over IPC exchange buffers, device-side flags (W > 1, one node)
+    def ipc_create(self, flat_numel: int = 0) -> bytes:
         n = _i64()
         check(lib().psgd_ipc_handle_bytes(ctypes.byref(n)))
         buf = (ctypes.c_uint8 * n.value)()
-        check(lib().psgd_ipc_create(self._h, buf))
+        check(lib().psgd_ipc_create(self._h, flat_numel, buf))
         return bytes(buf)
 
     def ipc_open(self, world: int, rank: int, handles: Sequence[bytes]) -> None:
@@ -228,11 +229,18 @@ class Plan:
         arr = (ctypes.c_uint8 * len(blob)).from_buffer_copy(blob)
         check(lib().psgd_ipc_open(self._h, world, rank, arr))
 
-    def ipc_publish(self, step: int, stream: int) -> None:
-        check(lib().psgd_ipc_publish(self._h, step, stream))
+    def aggregate_ipc(self, grads, out_ptr: int, step: int, flat, unc, flat_out: int, stream: int) -> None:
+        check(lib().psgd_aggregate_ipc(self._h, grads, out_ptr, step, flat._h if flat else None, unc, flat_out,
+                                       stream))
 
-    def ipc_sum(self, step: int, stream: int) -> None:
-        check(lib().psgd_ipc_sum(self._h, step, stream))
+    def ipc_status(self) -> bool:
+        """True if a device-side wait timed out since the last call (synchronous)."""
+        v = _i32()
+        check(lib().psgd_ipc_status(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
+    def ipc_close(self) -> None:
+        check(lib().psgd_ipc_close(self._h))
 
     def fused_final(self, step: int, aggregate: bool = True) -> int:
         """Nonzero when the last iteration of ``step`` runs fused with the final pass: 2 in the

@@ -75,6 +75,11 @@ constexpr int kProjRows = kFinRowsMax;
 // G - G X X^T (reference powersgd.py:185-230 with I = 2): the row pass needs X alone, no error
 // feedback term per element. The P state the reference keeps is P_1 = G X - P_0 R'^T (X^T X
 // = I), formed per row from the row sum.
+// Rank 1 (PJ, R = 1): the joint group norm N makes X = Q_0 / N orthonormal only over the whole
+// shape group, so X^T X = 1 fails per matrix. With c = Q_0,i . X = ||Q_0,i||^2 / N the
+// reference's output P_0 Q_0^T + P_1 X^T is exactly s X^T per row, s = G X + (N - c) P_0, its
+// residual G - s X^T, and its P state G X - c P_0 (single-matrix groups: N = c, the pure
+// projection). c comes from the even reduction's per-item sums of squares of the matrix.
 template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PJ = false>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
                                                float* red, float* rqs = nullptr) {
@@ -139,6 +144,11 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     // (rank-1 plans only: fused_norm, psgd_plan.cpp; compile-time false above rank 1)
     const bool norm = R == 1 && a.ss_in != nullptr;
     const float dn = norm ? group_norm_ss(a.ss_in, a.grng_in, d.group) : 1.f;
+    float cfac = 0.f, kfac = 0.f;  // rank-1 projection: c and N - c of this matrix
+    if constexpr (PJ && R == 1) {
+        cfac = range_ss(a.ss_in, a.mrng_in, t.mat) / dn;
+        kfac = dn - cfac;
+    }
     if (norm && t.chunk == 0) {  // row block 0 publishes this matrix's normalised in-factor
         for (int64_t e = tid; e < d.m * r; e += NT) {
             const float v = X[e] / dn;
@@ -153,7 +163,10 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     if constexpr (PJ) {
         if (tid < R * R) {
             const int c = tid / R, l = tid - (tid / R) * R;
-            rqs[tid] = (c < r && l < r) ? a.proj_r[d.qoff + c * r + l] : 0.f;
+            if constexpr (R == 1)
+                rqs[tid] = cfac;
+            else
+                rqs[tid] = (c < r && l < r) ? a.proj_r[d.qoff + c * r + l] : 0.f;
         }
         const int nst = int(row_end - row0) * R;  // the plan keeps row blocks <= kProjRows rows
         for (int e = tid; e < nst; e += NT) {
@@ -320,6 +333,9 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             }
                             a.yloc[e] = y;
                             a.state[e] = y;
+                            if constexpr (!PJ) {  // the exchange (W > 1) never takes the projection form
+                                if (a.xout) a.xout[e] = y;
+                            }
                         }
                 }
         }
@@ -330,6 +346,10 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
             for (int c = 0; c < R; ++c) pr[c] = c < r ? dot[u][c] : 0.f;
             const bool valid = ib + u < row_end;
+            if constexpr (PJ && R == 1) {  // s = G X + (N - c) P_0 (every thread of the row group)
+                const int li = valid ? int(ib + u - row0) : 0;
+                pr[0] = fmaf(kfac, rqs[R * R + li * R], pr[0]);
+            }
             const uint32_t rowe = uint32_t((ib + u) * int64_t(m));
 #pragma unroll
             for (int s = 0; s < SMAX; ++s) {
@@ -411,10 +431,13 @@ __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
     final_odd_block<T, R, K, SMAX, false>(a);
 }
 
+#ifndef PSGD_PROJ1_WPE
+#define PSGD_PROJ1_WPE 1
+#endif
 // Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
 // CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
 template <typename T, int R, int SMAX>
-__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : 1))) void k_final_proj(
+__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : R == 1 ? PSGD_PROJ1_WPE : 1))) void k_final_proj(
     FinalArgs a) {
     final_odd_block<T, R, 0, SMAX, true>(a);
 }
@@ -509,9 +532,7 @@ hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* wa
 // the instance that would run (the plan only fuses at >= 2).
 template <typename T, int R, int SMAX>
 hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
-    if constexpr (R == 2 || R == 4) {
-        if (nres == kFinProj) return launch_final_k<T, R, SMAX, 0, true>(a, ntiles, s, waves);
-    }
+    if (nres == kFinProj) return launch_final_k<T, R, SMAX, 0, true>(a, ntiles, s, waves);
     switch (nres) {
         case 0: return launch_final_k<T, R, SMAX, 0>(a, ntiles, s, waves);
         case 1: return launch_final_k<T, R, SMAX, 1>(a, ntiles, s, waves);
@@ -535,7 +556,8 @@ hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, 
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
     if constexpr (R <= 2) {
         if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
-        if (smax <= 12 && nres <= 1) {
+        if (smax <= 12 && (nres <= 1 || nres == kFinProj)) {
+            if (nres == kFinProj) return launch_final_k<T, R, 12, 0, true>(a, ntiles, s, waves);
             return nres == 0 ? launch_final_k<T, R, 12, 0>(a, ntiles, s, waves)
                              : launch_final_k<T, R, 12, 1>(a, ntiles, s, waves);
         }

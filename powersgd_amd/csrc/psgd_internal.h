@@ -193,6 +193,8 @@ struct ReduceArgs {
     // its output rows (kGramStride fp64 entries, rank gram_r in {2, 4}), or null
     double* gram;
     int32_t gram_r;
+    float* xout;         // one-shot exchange (psgd_aggregate_ipc): the local factor also goes to
+                         // this rank's exchange slot (same offsets as `state`), or null
 };
 
 constexpr int kGramStride = 10;  // fp64 Gram entries per reduction item (rank <= 4)
@@ -235,7 +237,10 @@ struct FinalArgs {
     // projection form (nres = kFinProj, see psgd_final.cuh): P_0 rows and R' per matrix
     const float* proj_p0;  // P layout
     const float* proj_r;   // Q layout: R' (r x r, row-major) at each matrix's qoff
-
+    // rank-1 projection form: per matrix [begin, end) of the even reduction's sum-of-squares
+    // items (ss_in), for ||Q_0,i||^2 of the matrix against the group norm
+    const int32_t* mrng_in;
+    float* xout;           // one-shot exchange: P local also to this rank's exchange slot, or null
 };
 // nres value selecting the projection form of the fused final pass (I = 2, world size 1)
 constexpr int kFinProj = 1000;
@@ -316,14 +321,28 @@ hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
 hipError_t launch_flat_pack_f64(const FlatArgs& a, hipStream_t s);
 
-// one-shot all-reduce over IPC-mapped exchange buffers (psgd_ipc_*)
+// One-shot all-reduce over IPC-mapped exchange buffers (psgd_aggregate_ipc). Every rank's
+// exchange buffer: kXchgHeader bytes of per-iteration epoch flags (uint64, one per iteration),
+// then two parities x iterations slots of xchg_slot floats each; the producer kernels (k_reduce,
+// k_final_odd, the flat pack) write the LOCAL factor into this rank's slot, and k_xchg raises
+// this rank's flag, waits (bounded) for every peer's flag and sums the W slots in rank order.
 constexpr int kMaxRanks = 64;
-struct IpcSumArgs {
-    const float* const* peers;  // device array: world exchange buffers, rank order
-    float* dst;
-    int64_t n;
-    int32_t world;
+constexpr int64_t kXchgHeader = 256;
+struct XchgArgs {
+    const char* const* peers;  // device array: the W exchange buffers (rank order, own included)
+    uint64_t* own_flag;        // this rank's flag of this iteration (its own buffer)
+    int64_t flag_off;          // byte offset of this iteration's flag in every buffer
+    int64_t slot_off;          // byte offset of this step/iteration's slot in every buffer
+    float* dst;                // SUM of the factors (the reference-visible state) ...
+    int64_t n;                 // ... n floats
+    float* flat_dst;           // SUM of the packed uncompressed tensors (last iteration) ...
+    int64_t flat_off;          // ... at slot + flat_off floats
+    int64_t nflat;
+    uint64_t epoch;            // step + 1
+    uint32_t spin_limit;       // polls (~0.25 us apart) before a wait gives up
+    int32_t world, rank;
+    int32_t* err;              // set to 1 when a wait timed out (psgd_ipc_status)
 };
-hipError_t launch_ipc_sum(const IpcSumArgs& a, hipStream_t s);
+hipError_t launch_xchg(const XchgArgs& a, hipStream_t s);
 
 }  // namespace psgd

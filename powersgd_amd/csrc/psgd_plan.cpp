@@ -442,12 +442,19 @@ struct psgd_plan {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
-    // one-shot IPC all-reduce of the last factor (psgd_ipc_*): this rank's exchange buffer
-    // (hipMalloc'd so that it can be exported) and the peers' opened mappings
-    float* ipc_buf = nullptr;
+    // one-shot IPC all-reduce (psgd_ipc_*, psgd_aggregate_ipc): this rank's exchange buffer
+    // (hipMalloc'd so that it can be exported: flags header + 2 parities x iters slots), the
+    // peers' opened mappings, the slot size (floats: factor region, then the flat region)
+    char* ipc_buf = nullptr;
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
-    size_t o_ipc_ptrs = 0;
+    int64_t ipc_slot = 0, ipc_flat_off = 0, ipc_flat_cap = 0;
+    size_t o_ipc_ptrs = 0, o_xerr = 0;
+    float* xout_now = nullptr;  // set per iteration by psgd_aggregate_ipc (exchange slot)
+    int64_t xslot_off(int64_t step, int it) const {  // byte offset of a slot in every buffer
+        return kXchgHeader + ((step & 1) * iters + it) * ipc_slot * int64_t(sizeof(float));
+    }
+    float* xslot(int64_t step, int it) const { return reinterpret_cast<float*>(ipc_buf + xslot_off(step, it)); }
     size_t o_rq = 0;  // R' of the last iteration's in-factor panels (projection form), Q layout
     // folded orthonormalisation of the projection form's Q panels (k_orth_chain): every Q unit
     // a single panel of exactly rbucket in {2, 4} columns; per-item Gram partials and per-unit
@@ -455,6 +462,8 @@ struct psgd_plan {
     bool qfold_ok = false;
     size_t o_gram = 0, o_uitems = 0;
     std::vector<int32_t> uitems, red_even_b, red_even_e;
+    std::vector<int32_t> mrng_even;  // per matrix [begin, end) of its even reduction items
+    size_t o_mrng = 0;
     bool qfold(int64_t step, bool agg) const { return qfold_ok && iters == 2 && proj_final(step, agg); }
 
     ~psgd_plan() {
@@ -464,7 +473,7 @@ struct psgd_plan {
         }
         for (size_t w = 0; w < ipc_peer.size(); ++w)
             if (ipc_peer[w] && int(w) != ipc_rank) (void)hipIpcCloseMemHandle(ipc_peer[w]);
-        if (ipc_buf) (void)hipFree(ipc_buf);
+        if (ipc_buf) (void)hipFree(ipc_buf);  // peers must have closed it first (psgd_ipc_close)
     }
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
@@ -691,6 +700,11 @@ struct psgd_plan {
             grng_even[2 * g + 1] = int32_t(red_even.size());
             grng_odd[2 * g + 1] = int32_t(red_odd.size());
         }
+        mrng_even.clear();
+        for (size_t i = 0; i < mats.size(); ++i) {
+            mrng_even.push_back(red_even_b[i]);
+            mrng_even.push_back(red_even_e[i]);
+        }
         // folded orthonormalisation: per Q unit (one matrix each) its even item range
         uitems.clear();
         if (qfold_ok) {
@@ -773,7 +787,10 @@ struct psgd_plan {
         // Projection form (psgd_final.cuh): two power iterations at world size 1, ranks 2 and 4,
         // the last iteration's in-factor orthonormalised by Cholesky-QR (which leaves R').
         // Same register-panel geometry as the K-term form, so both can share the tile list.
-        if (fuse_mode != 0 && small && iters == 2 && (rbucket == 2 || rbucket == 4) && orth_chol &&
+        // Rank 1 (the joint group norm folded into the kernels, psgd_aggregate): the same form with
+        // the per-matrix correction of psgd_final.cuh; it needs the folded norm's sums of squares.
+        const bool proj_r1 = rbucket == 1 && env_int("PSGD_FUSE_NORM", 1) != 0 && env_int("PSGD_FIN_PROJ1", 1) != 0;
+        if (fuse_mode != 0 && small && iters == 2 && (((rbucket == 2 || rbucket == 4) && orth_chol) || proj_r1) &&
             env_int("PSGD_FIN_PROJ", 1) != 0)
             fin_proj = fits(kFinProj);
         fin_smax = 0;
@@ -869,6 +886,7 @@ int psgd_plan::upload_tiles() const {
     if (int st = upload(dev<void>(o_grng_ss0), grng_ss0.data(), grng_ss0.size() * sizeof(int32_t))) return st;
     if (qfold_ok)
         if (int st = upload(dev<void>(o_uitems), uitems.data(), uitems.size() * sizeof(int32_t))) return st;
+    if (int st = upload(dev<void>(o_mrng), mrng_even.data(), mrng_even.size() * sizeof(int32_t))) return st;
     return PSGD_OK;
 }
 
@@ -1126,11 +1144,13 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
     p->o_ipc_ptrs = carve(size_t(kMaxRanks) * sizeof(void*));
+    p->o_xerr = carve(sizeof(int32_t));
     p->o_rq = carve(size_t(std::max<int64_t>(p->fmax, 1)) * sizeof(float));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_grng_even = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
     p->o_grng_odd = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    p->o_mrng = carve(std::max<size_t>(2 * p->mats.size(), 1) * sizeof(int32_t));
     p->ss_stride = size_t(std::max<int64_t>(p->red_even_cap, p->red_odd_cap));
     p->o_ss = carve(2 * std::max<size_t>(p->ss_stride, 1) * sizeof(float));
     p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_cap, 1)) * sizeof(float));
@@ -1262,8 +1282,10 @@ static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEv
     if (!p->timing) return PSGD_OK;
     if (p->ev_used == p->ev_pool.size()) {
         std::pair<hipEvent_t, hipEvent_t> e;
-        PSGD_HIP(hipEventCreate(&e.first));
-        PSGD_HIP(hipEventCreate(&e.second));
+        // no system-scope fence: a system-scope release writes back the L2s around the timed
+        // kernel (~5.6 us of idle queue per event in the traces) that a plain step never pays
+        PSGD_HIP(hipEventCreateWithFlags(&e.first, hipEventDisableSystemFence));
+        PSGD_HIP(hipEventCreateWithFlags(&e.second, hipEventDisableSystemFence));
         p->ev_pool.push_back(e);
     }
     *ev = &p->ev_pool[p->ev_used++];
@@ -1404,6 +1426,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         fa.write_out = write_out ? 1 : 0;
         fa.yloc = p->hist(1, it);
         fa.state = out;
+        fa.xout = p->xout_now;
         if (fused) {
             fa.ss_in = prev_ss;  // the in-factor Q came from an even iteration's reduction
             fa.grng_in = prev_grng;
@@ -1411,9 +1434,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
             fa.hx = p->hist(0, it);
         }
         const int nfin = sp.fin[1] - sp.fin[0];
-        if (proj) {  // no error-feedback terms: P_0 and R' only
+        if (proj) {  // no error-feedback terms: P_0 and R' only (rank 1: P_0 and the matrix's c)
             fa.proj_p0 = p->hist(0, 0);
             fa.proj_r = p->dev<float>(p->o_rq);
+            fa.mrng_in = p->dev<int32_t>(p->o_mrng);
             fill_terms(p, step, 0, fa.res);
             fa.nres = kFinProj;
         }
@@ -1485,6 +1509,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     }
     // ss_out is indexed by the launch's block (item) index: offset like the item list
     if (fused_norm(p, fuse, it + 1) && it + 1 < p->iters) ra.ss_out = ss + size_t(it & 1) * p->ss_stride + rr[0];
+    ra.xout = p->xout_now;
     if (qf && even && it + 2 == p->iters) {  // the Q panels' Gram for k_orth_chain
         ra.gram = p->dev<double>(p->o_gram) + size_t(rr[0]) * kGramStride;
         ra.gram_r = p->rbucket;
@@ -1628,12 +1653,22 @@ int psgd_ipc_handle_bytes(int64_t* bytes) {
     return PSGD_OK;
 }
 
-int psgd_ipc_create(psgd_plan* p, void* handle_out) {
+int psgd_ipc_create(psgd_plan* p, int64_t flat_numel, void* handle_out) {
     if (!p || !handle_out) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (p->f64()) return fail(PSGD_ERR_DTYPE, "the IPC all-reduce takes fp32/bf16 plans");
+    if (flat_numel < 0) return fail(PSGD_ERR_VALUE, "negative flat size");
+    if (p->ipc_buf) return fail(PSGD_ERR_STATE, "exchange buffer already created");
     DevScope scope(p->device);
-    if (!p->ipc_buf) PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->ipc_buf), size_t(std::max<int64_t>(p->fmax, 1)) * 4));
+    auto a64 = [](int64_t x) { return (x + 63) & ~int64_t(63); };
+    p->ipc_flat_off = a64(std::max<int64_t>(p->fmax, 1));
+    p->ipc_flat_cap = flat_numel;
+    p->ipc_slot = p->ipc_flat_off + a64(flat_numel);
+    const size_t bytes = size_t(kXchgHeader) + size_t(2 * p->iters * p->ipc_slot) * sizeof(float);
+    PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->ipc_buf), bytes));
+    PSGD_HIP(hipMemset(p->ipc_buf, 0, bytes));  // flags at epoch 0
+    PSGD_HIP(hipMemset(p->dev<int32_t>(p->o_xerr), 0, sizeof(int32_t)));
+    PSGD_HIP(hipDeviceSynchronize());  // zeroed before any peer can open and poll it
     PSGD_HIP(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), p->ipc_buf));
     return PSGD_OK;
 }
@@ -1641,47 +1676,51 @@ int psgd_ipc_create(psgd_plan* p, void* handle_out) {
 int psgd_ipc_open(psgd_plan* p, int32_t world, int32_t rank, const void* handles) {
     if (!p || !handles) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->ipc_buf) return fail(PSGD_ERR_STATE, "psgd_ipc_create first");
+    if (!p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "peers already open (psgd_ipc_close first)");
     if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return fail(PSGD_ERR_VALUE, "bad world/rank");
     DevScope scope(p->device);
     const auto* h = static_cast<const hipIpcMemHandle_t*>(handles);
-    p->ipc_peer.assign(size_t(world), nullptr);
-    p->ipc_world = world;
-    p->ipc_rank = rank;
+    std::vector<void*> peer(size_t(world), nullptr);
     for (int w = 0; w < world; ++w) {
         if (w == rank) {
-            p->ipc_peer[w] = p->ipc_buf;
+            peer[w] = p->ipc_buf;
             continue;
         }
-        PSGD_HIP(hipIpcOpenMemHandle(&p->ipc_peer[w], h[w], hipIpcMemLazyEnablePeerAccess));
+        const hipError_t e = hipIpcOpenMemHandle(&peer[w], h[w], hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            for (int v = 0; v < w; ++v)
+                if (v != rank && peer[v]) (void)hipIpcCloseMemHandle(peer[v]);
+            return fail(PSGD_ERR_DEVICE, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        }
     }
+    p->ipc_peer = peer;
+    p->ipc_world = world;
+    p->ipc_rank = rank;
     return upload(p->dev<void>(p->o_ipc_ptrs), p->ipc_peer.data(), size_t(world) * sizeof(void*));
 }
 
-// the last iteration's LOCAL factor (history slot 1) -> this rank's exchange buffer
-int psgd_ipc_publish(psgd_plan* p, int64_t step, void* stream) {
+int psgd_ipc_close(psgd_plan* p) {
     if (!p) return fail(PSGD_ERR_VALUE, "null plan");
-    if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+    if (p->ipc_peer.empty()) return PSGD_OK;
     DevScope scope(p->device);
-    const int last = p->iters - 1;
-    const int64_t n = p->even(step, last) ? p->qtot : p->ptot;
-    PSGD_HIP(hipMemcpyAsync(p->ipc_buf, p->hist(1, last), size_t(n) * 4, hipMemcpyDeviceToDevice,
-                            static_cast<hipStream_t>(stream)));
+    PSGD_HIP(hipDeviceSynchronize());  // no kernel of this rank still reads a peer buffer
+    for (size_t w = 0; w < p->ipc_peer.size(); ++w)
+        if (p->ipc_peer[w] && int(w) != p->ipc_rank) (void)hipIpcCloseMemHandle(p->ipc_peer[w]);
+    p->ipc_peer.clear();
+    p->ipc_world = 0;
+    p->ipc_rank = -1;
     return PSGD_OK;
 }
 
-// the last iteration's out-factor state <- SUM over the ranks' exchange buffers (one-shot)
-int psgd_ipc_sum(psgd_plan* p, int64_t step, void* stream) {
-    if (!p) return fail(PSGD_ERR_VALUE, "null plan");
-    if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+int psgd_ipc_status(psgd_plan* p, int32_t* timed_out) {
+    if (!p || !timed_out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     DevScope scope(p->device);
-    const int last = p->iters - 1;
-    const bool e = p->even(step, last);
-    IpcSumArgs a{};
-    a.peers = p->dev<const float* const>(p->o_ipc_ptrs);
-    a.dst = e ? p->Q : p->P;
-    a.n = e ? p->qtot : p->ptot;
-    a.world = p->ipc_world;
-    PSGD_HIP(launch_ipc_sum(a, static_cast<hipStream_t>(stream)));
+    int32_t v = 0;
+    PSGD_HIP(hipDeviceSynchronize());
+    PSGD_HIP(hipMemcpy(&v, p->dev<int32_t>(p->o_xerr), sizeof(v), hipMemcpyDeviceToHost));
+    if (v) PSGD_HIP(hipMemset(p->dev<int32_t>(p->o_xerr), 0, sizeof(int32_t)));
+    *timed_out = v;
     return PSGD_OK;
 }
 
@@ -2006,6 +2045,68 @@ int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t ste
                                     last && has_flat ? static_cast<float*>(flat_out) : nullptr,
                                     last && has_flat ? size_t(f->total) : 0, s))
             return st;
+    }
+    return decompress_impl(p, grads, out, step, world, s, false);
+}
+
+
+// World size W over the IPC exchange (include/psgd.h): per iteration the codec kernels (the
+// reduction or fused final pass also writes the local factor into this rank's exchange slot),
+// then k_xchg (flag, bounded wait for the peers' flags, rank-order SUM into the state buffer; the
+// last one also sums the uncompressed tensors packed /W into flat_out), then the output pass.
+// Nothing leaves the stream: no host barrier, no host synchronisation.
+int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f, void* const* unc,
+                       void* flat_out, void* stream) {
+    if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
+    if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
+    const bool has_flat = f && f->total > 0;
+    if (has_flat) {
+        if (!unc || !flat_out) return fail(PSGD_ERR_VALUE, "null argument");
+        if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
+        if (f->dtype != PSGD_F32) return fail(PSGD_ERR_DTYPE, "psgd_aggregate_ipc packs fp32 uncompressed tensors");
+        if (f->total > p->ipc_flat_cap) return fail(PSGD_ERR_VALUE, "flat tensors exceed the exchange buffer (psgd_ipc_create)");
+    }
+    DevScope scope(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int world = p->ipc_world;
+    const int last = p->iters - 1;
+    static const uint32_t spin = uint32_t(std::min<int64_t>(env_int("PSGD_IPC_SPIN", int64_t(1) << 26), 0xffffffffLL));
+    // x / W into this rank's last slot: inside the first even product's launch when the step
+    // starts even, else its own launch
+    FlatArgs fa{};
+    const bool fold = has_flat && p->even(step, 0);
+    float* flat_slot = p->xslot(step, last) + p->ipc_flat_off;
+    if (has_flat) {
+        if (int st = flat_args(f, unc, flat_slot, world, s, &fa)) return st;
+        if (!fold) PSGD_HIP(launch_flat_pack(f->dtype, fa, s));
+    }
+    for (int it = 0; it < p->iters; ++it) {
+        p->xout_now = p->xslot(step, it);
+        const int st = compress_impl(p, grads, step, it, s, false, false, fold ? &fa : nullptr);
+        p->xout_now = nullptr;
+        if (st) return st;
+        const bool e = p->even(step, it);
+        XchgArgs xa{};
+        xa.peers = p->dev<const char* const>(p->o_ipc_ptrs);
+        xa.own_flag = reinterpret_cast<uint64_t*>(p->ipc_buf) + it;
+        xa.flag_off = int64_t(it) * int64_t(sizeof(uint64_t));
+        xa.slot_off = p->xslot_off(step, it);
+        xa.dst = e ? p->Q : p->P;
+        xa.n = e ? p->qtot : p->ptot;
+        if (it == last && has_flat) {
+            xa.flat_dst = static_cast<float*>(flat_out);
+            xa.flat_off = p->ipc_flat_off;
+            xa.nflat = f->total;
+        }
+        xa.epoch = uint64_t(step) + 1;
+        xa.spin_limit = spin;
+        xa.world = world;
+        xa.rank = p->ipc_rank;
+        xa.err = p->dev<int32_t>(p->o_xerr);
+        PSGD_HIP(launch_xchg(xa, s));
     }
     return decompress_impl(p, grads, out, step, world, s, false);
 }

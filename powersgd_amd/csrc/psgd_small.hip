@@ -1842,6 +1842,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         if (e < cnt) {
             a.yloc[dbase + e] = t;
             a.state[dbase + e] = t;
+            if (a.xout) a.xout[dbase + e] = t;
             sq = fmaf(t, t, sq);
             tv[j] = t;
         }
@@ -1897,24 +1898,79 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- one-shot all-reduce
-// SUM over the ranks' exchange buffers, read directly through IPC mappings (each rank reads
-// all W buffers once: the one-shot form of the reference's all_reduce, powersgd.py:204-209).
-// Fixed rank order, so every rank computes bitwise the same sum. Peer reads are system-scope
-// relaxed atomic loads: they bypass the non-coherent caches, whatever a previous step left there.
-__global__ __launch_bounds__(kBlock) void k_ipc_sum(IpcSumArgs a) {
-    const int64_t stride = int64_t(gridDim.x) * kBlock;
-    for (int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x; e < a.n; e += stride) {
-        float s = __hip_atomic_load(a.peers[0] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        for (int w = 1; w < a.world; ++w)
-            s += __hip_atomic_load(a.peers[w] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        a.dst[e] = s;
+// The reference's SUM all-reduce of an out-factor (powersgd.py:204-209), one node, one
+// process per GPU, stream-ordered with no host round trip: the kernels before this one left the
+// LOCAL factor in this rank's exchange slot (their completion on this stream makes it visible
+// device-wide); workgroup 0 raises this rank's epoch flag for the iteration (system-scope
+// release), then every workgroup polls the peers' flags (system-scope loads, bounded: a peer
+// that never arrives sets a.err instead of hanging the queue) and sums its share of the W slots
+// in rank order, so every rank computes bitwise the same values. Peer data is read with
+// system-scope loads: no stale line a previous step left in this XCD's caches can be hit.
+// System-scope (sc0 | sc1) 16-byte loads: they miss in every non-coherent cache level.
+constexpr int kSysAux = 17;
+constexpr int kXchgUnroll = 8;  // peers whose loads are in flight together
+
+__device__ __forceinline__ void xchg_sum_quad(const XchgArgs& a, int64_t src_byte, uint32_t lim, float (&s)[4]) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    for (int w0 = 0; w0 < a.world; w0 += kXchgUnroll) {
+        v4u v[kXchgUnroll];
+#pragma unroll
+        for (int u = 0; u < kXchgUnroll; ++u) {
+            const bool on = w0 + u < a.world;  // past the last peer: an empty descriptor, no access
+            const rsrc_t rs = make_rsrc(a.peers[on ? w0 + u : w0] + a.slot_off, on ? lim : 0u);
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, uint32_t(src_byte), 0, kSysAux);
+        }
+#pragma unroll
+        for (int u = 0; u < kXchgUnroll; ++u)
+            if (w0 + u < a.world)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float x = __uint_as_float(v[u][j]);
+                    s[j] = w0 + u == 0 ? x : s[j] + x;  // rank order
+                }
     }
 }
 
-hipError_t launch_ipc_sum(const IpcSumArgs& a, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
-    const int64_t blocks = (a.n + kBlock - 1) / kBlock;
-    k_ipc_sum<<<int(blocks < 1024 ? blocks : 1024), kBlock, 0, s>>>(a);
+__global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0)
+        __hip_atomic_store(a.own_flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid < a.world && tid != a.rank) {  // lane w polls peer w: the W round trips overlap
+        const uint64_t* f = reinterpret_cast<const uint64_t*>(a.peers[tid] + a.flag_off);
+        uint32_t spins = 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
+            if (++spins > a.spin_limit) {
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(10);
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    __syncthreads();
+    // quads of the factor, then quads of the flat region; buffer bounds zero-fill a ragged tail
+    const int64_t qf = (a.n + 3) / 4, qt = qf + (a.nflat + 3) / 4;
+    const int64_t stride = int64_t(gridDim.x) * kBlock;
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + tid; q < qt; q += stride) {
+        const bool fac = q < qf;
+        const int64_t e0 = fac ? 4 * q : 4 * (q - qf);  // element index in dst / flat_dst
+        const int64_t cnt = fac ? a.n : a.nflat;
+        const int64_t base = fac ? 0 : a.flat_off;
+        const uint32_t lim = uint32_t((base + cnt) * int64_t(sizeof(float)));
+        float s[4];
+        xchg_sum_quad(a, (base + e0) * int64_t(sizeof(float)), lim, s);
+        float* d = fac ? a.dst : a.flat_dst;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e0 + j < cnt) d[e0 + j] = s[j];
+    }
+}
+
+hipError_t launch_xchg(const XchgArgs& a, hipStream_t s) {
+    const int64_t quads = (a.n + 3) / 4 + (a.nflat + 3) / 4;
+    const int64_t blocks = (quads + kBlock - 1) / kBlock;
+    // at least one workgroup (it raises the flag), at most one per CU
+    k_xchg<<<int(blocks < 1 ? 1 : blocks < 256 ? blocks : 256), kBlock, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -245,6 +245,16 @@ __device__ __forceinline__ float group_norm_ss(const float* ss, const int32_t* g
     return nrm > 1e-16f ? nrm : 1e-16f;
 }
 
+// Plain sum of the sum-of-squares partials [rng[2 i], rng[2 i + 1]) (same wave order as
+// group_norm_ss; one matrix's items for the rank-1 projection form)
+__device__ __forceinline__ float range_ss(const float* ss, const int32_t* rng, int i) {
+    const int lane = threadIdx.x & 63;
+    const int b = rng[2 * i], e = rng[2 * i + 1];
+    float acc = 0.f;
+    for (int k = b + lane; k < e; k += 64) acc += ss[k];
+    return wave_allsum(acc);
+}
+
 // One flat-pack item (kFlatItem consecutive elements of one uncompressed tensor; reference
 // powersgd.py:22-31 + utils.py:6-10, :43-49): flat = x / W (division, as div_; an exact
 // copy at W = 1), then x = 0. NT threads; one read + two writes per element.

@@ -161,8 +161,7 @@ class PowerSGD(Aggregator):
         unc_shapes = [t.shape for t, c in zip(params, self.is_compressed_mask) if not c]
         self._unc = _FlatEntry(unc_shapes, p._code, p.dtype, p.device) if unc_shapes else None
         # one fp32 collective can carry factor + uncompressed values (fp32 gradients only)
-        self._merge_ok = (p.dtype == torch.float32 and os.environ.get("PSGD_MERGE_ALLREDUCE", "1") != "0"
-                          and os.environ.get("PSGD_IPC_ALLREDUCE") != "1")
+        self._merge_ok = p.dtype == torch.float32 and os.environ.get("PSGD_MERGE_ALLREDUCE", "1") != "0"
         # _merge order: position of tensor i in (compressed outputs + uncompressed outputs)
         nc = sum(self.is_compressed_mask)
         ic, iu, self._order = 0, nc, []
@@ -177,11 +176,15 @@ class PowerSGD(Aggregator):
         if not isinstance(gradients, list):
             gradients = list(gradients)
         self._table.fill(gradients)  # reference _split :76-84 + the checks its torch ops make
-        comm = self._powersgd._rccl_comm() if is_distributed() else None
-        if comm is not None:
-            # world size W, RCCL: the whole step in one library call on the codec's stream; the
-            # uncompressed tensors (fp32) ride in the last factor collective
-            codec, u = self._powersgd, self._unc
+        codec = self._powersgd
+        ipc = is_distributed() and codec._ipc_mode()
+        comm = codec._rccl_comm() if is_distributed() and not ipc else None
+        if ipc or comm is not None:
+            # world size W, RCCL or the IPC exchange: the whole step in one library call on the
+            # codec's stream; the uncompressed tensors (fp32) ride in the last factor's exchange
+            u = self._unc
+            if ipc:
+                codec._ipc_setup(u.numel if u is not None and u.dtype == torch.float32 else 0)
             if u is not None and u.dtype == torch.float32:
                 unc = u.slab.get()
                 outs = codec._aggregate_table(self._table.comp_addr(),
@@ -293,7 +296,7 @@ class BasicPowerSGD(Aggregator):
         self._p_comm: Optional[torch.Tensor] = None
         self._q_comm: Optional[torch.Tensor] = None
         self._buckets: Optional[List[tuple]] = None  # W > 1: (p_off, p_len, q_off, q_len) per bucket
-        self._ipc_open = False  # W > 1 with PSGD_IPC_ALLREDUCE=1: peers' exchange buffers mapped
+        self._ipc_open = False  # W > 1 with PSGD_COMM=ipc: peers' exchange buffers mapped
         self._comm = None  # W > 1 over RCCL: the library's own communicator (_rccl_comm)
 
     def aggregate(self, gradients: List[torch.Tensor]) -> List[torch.Tensor]:
@@ -303,16 +306,64 @@ class BasicPowerSGD(Aggregator):
         self._table.fill(gradients)  # dtype / device / shape / contiguity checks + pointers
         return self._aggregate_table(self._table.comp_addr())
 
+    def _ipc_mode(self) -> bool:
+        """PSGD_COMM=ipc (or PSGD_IPC_ALLREDUCE=1): every factor all-reduce of a step runs as a
+        one-shot sum over IPC-mapped exchange buffers with device-side flags (psgd_aggregate_ipc;
+        one node, one process per GPU). fp32/bf16 plans; any torch.distributed backend carries
+        the one-off handle exchange."""
+        mode = os.environ.get("PSGD_COMM", "rccl")
+        if os.environ.get("PSGD_IPC_ALLREDUCE") == "1":
+            mode = "ipc"
+        return mode == "ipc" and self.dtype != torch.float64
+
+    def _ipc_setup(self, flat_numel: int = 0) -> None:
+        """Collective, once: create this rank's exchange buffer (room for ``flat_numel``
+        uncompressed values), all-gather the IPC handles and open the peers' buffers."""
+        if self._ipc_open:
+            return
+        dist = torch.distributed
+        world = dist.get_world_size()
+        handle = self._plan.ipc_create(flat_numel)
+        handles: List = [None] * world
+        dist.all_gather_object(handles, handle)
+        err = None
+        try:
+            self._plan.ipc_open(world, dist.get_rank(), handles)
+        except RuntimeError as e:
+            err = str(e)
+        # collective outcome: one rank failing to map a peer must not leave the others polling
+        # flags it will never raise
+        errs: List = [None] * world
+        dist.all_gather_object(errs, err)
+        bad = [(r, e) for r, e in enumerate(errs) if e is not None]
+        if bad:
+            if err is None:
+                self._plan.ipc_close()
+            raise RuntimeError(f"IPC exchange setup failed on rank(s) {bad}")
+        self._ipc_open = True
+
+    def ipc_status(self) -> bool:
+        """True if a device-side exchange wait timed out since the last call (synchronous)."""
+        return self._ipc_open and self._plan.ipc_status()
+
+    def close_ipc(self) -> None:
+        """Collective teardown of the IPC exchange: unmap the peers' buffers, then a barrier, so
+        that no rank frees its exchange buffer while a peer still maps it (include/psgd.h)."""
+        if self._ipc_open:
+            self._plan.ipc_close()
+            self._ipc_open = False
+            torch.distributed.barrier()
+
     def _rccl_comm(self) -> Optional["_lib.Comm"]:
         """World size > 1 on the NCCL (RCCL) backend: a communicator the library drives itself on
         the codec's stream (psgd_comm_init; the id travels over the default process group), so a
         whole step is one call (psgd_aggregate_comm). None on gloo, for fp64 plans, with
-        PSGD_COMM=torch (the torch.distributed path below) or PSGD_IPC_ALLREDUCE=1."""
+        PSGD_COMM=torch (the torch.distributed path below) or PSGD_COMM=ipc."""
         if self._comm is None:
             self._comm = False
             dist = torch.distributed
             if (os.environ.get("PSGD_COMM", "rccl") == "rccl" and dist.get_backend() == "nccl"
-                    and self.dtype != torch.float64 and os.environ.get("PSGD_IPC_ALLREDUCE") != "1"):
+                    and self.dtype != torch.float64 and not self._ipc_mode()):
                 world, rank = dist.get_world_size(), dist.get_rank()
                 obj = [_lib.comm_unique_id() if rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
@@ -350,17 +401,18 @@ class BasicPowerSGD(Aggregator):
         out_ptr = self._slab.data_ptr()
         stream = _stream(self.device)
         step = self.step_counter
-        comm = self._rccl_comm() if is_distributed() and last_comm is None else None
-        if comm is not None:
+        ipc = is_distributed() and last_comm is None and self._ipc_mode()
+        comm = self._rccl_comm() if is_distributed() and last_comm is None and not ipc else None
+        if ipc:
+            self._ipc_setup(0)
+            f = flat if flat is not None else (None, None, 0)
+            self._plan.aggregate_ipc(ptrs, out_ptr, step, f[0], f[1], f[2], stream)
+        elif comm is not None:
             f = flat if flat is not None else (None, None, 0)
             self._plan.aggregate_comm(ptrs, out_ptr, step, f[0], f[1], f[2], comm, stream)
         elif is_distributed():
             world = torch.distributed.get_world_size()
             iters = self.config.num_iters_per_step
-            if os.environ.get("PSGD_IPC_ALLREDUCE") == "1" and last_comm is None and self.dtype != torch.float64:
-                self._aggregate_ipc(ptrs, out_ptr, step, world, stream)
-                self.step_counter += 1
-                return outs
             if self._buckets is None:
                 self._setup_buckets()
             if len(self._buckets) > 1:
@@ -379,33 +431,6 @@ class BasicPowerSGD(Aggregator):
             self._plan.aggregate(ptrs, out_ptr, step, stream)
         self.step_counter += 1
         return outs
-
-    def _aggregate_ipc(self, ptrs: int, out_ptr: int, step: int, world: int, stream: int) -> None:
-        """Prototype: the LAST iteration's factor all-reduce as a one-shot sum over IPC mappings
-        (each rank reads every rank's local factor directly, psgd_ipc_*), the earlier iterations
-        as the reference's all_reduce. The two host barriers per step order the exchange buffers
-        across processes; on one node they would become device-side flags."""
-        dist = torch.distributed
-        if not self._ipc_open:
-            handle = self._plan.ipc_create()
-            handles: List = [None] * world
-            dist.all_gather_object(handles, handle)
-            self._plan.ipc_open(world, dist.get_rank(), handles)
-            self._ipc_open = True
-        iters = self.config.num_iters_per_step
-        for it in range(iters):
-            self._plan.compress(ptrs, step, it, stream)
-            if it < iters - 1:
-                buf = self._qs_buffer if self._plan.out_factor(step, it) == 0 else self._ps_buffer
-                dist.all_reduce(buf)  # SUM of the local factors, reference :207
-        cur = torch.cuda.current_stream(self.device)
-        cur.synchronize()
-        dist.barrier()  # every rank has finished reading the exchange buffers of the previous step
-        self._plan.ipc_publish(step, stream)
-        cur.synchronize()
-        dist.barrier()  # every rank's local factor is in its exchange buffer
-        self._plan.ipc_sum(step, stream)  # one-shot SUM over the ranks (reference :207)
-        self._plan.decompress(ptrs, out_ptr, step, world, stream)
 
     def _setup_buckets(self) -> None:
         """Cut the shape groups into up to PSGD_BUCKETS (default 4) consecutive buckets of about

@@ -10,7 +10,7 @@ registers. These tests pin it three ways:
 * the world-size > 1 code path (psgd_compress writes the residual, psgd_decompress writes
   only the output with k_lowrank_out) driven at world size 1 through the C ABI, against
   the single-call psgd_aggregate.
-Two-iteration rank-2/4 plans take the projection form in psgd_aggregate (output G X X^T,
+Two-iteration rank-1/2/4 plans take the projection form in psgd_aggregate (output G X X^T,
 residual G - G X X^T, P state G X - P_0 R'^T; exact algebra for I = 2 at world size 1, see
 psgd_final.cuh): checked against the oracle at the same 1e-5, and against the K-term form
 (PSGD_FIN_PROJ=0) through the unfused comparison.
@@ -84,7 +84,7 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         form = fused._powersgd._plan.fused_final(t)
         n_fused += bool(form)
         if form:  # 2 = projection form: exactly the two-iteration rank-2/4 register-panel plans
-            assert (form == 2) == (proj and mode == 2 and iters == 2 and rank in (2, 4)), (form, t)
+            assert (form == 2) == (proj and mode == 2 and iters == 2 and rank in (1, 2, 4)), (form, t)
         ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 0.5, iters, 0)
         ora.codec.p_flat.copy_(fused._powersgd._ps_buffer.cpu())
         ora.codec.q_flat.copy_(fused._powersgd._qs_buffer.cpu())
@@ -110,7 +110,7 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
         plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
     expect_odd_last = sum(((t * iters + iters - 1) % 2) == 1 for t in range(3))
-    projection = proj and mode == 2 and iters == 2 and rank in (2, 4)
+    projection = proj and mode == 2 and iters == 2 and rank in (1, 2, 4)
     if narrow or (rank == 1 and iters <= 2) or projection:  # configurations that must fuse
         assert n_fused == expect_odd_last, (n_fused, expect_odd_last)
 
@@ -169,3 +169,16 @@ def test_split_calls_match_aggregate(rank, iters):
             k += 1
             assert _rel(oa[i], ob, g) <= 1e-6, (t, i, "out")
             assert _rel(ga[i], gb[i], g) <= 1e-6, (t, i, "res")
+
+
+@pytest.mark.parametrize("cfg,form", [("cfg1_1024sq_r1", 2), ("cfg2_resnet50_r1", 2), ("cfg3_resnet50_r4", 2),
+                                      ("cfg5_lstm_r1_i4", 1)])
+def test_baseline_configs_take_the_fused_forms(cfg, form):
+    """The BASELINE configurations run the fused final pass at world size 1 (K-term form, or the
+    projection form at rank 4): an instance that stops fitting two waves per SIMD without scratch
+    (e.g. after a kernel change) silently falls back to the unfused kernels — caught here."""
+    from powersgd_amd.workloads import CONFIGS
+
+    c = CONFIGS[cfg]
+    psgd = PowerSGD([torch.zeros(s, device=DEV) for s in c["shapes"]], Config(c["rank"], c["mcr"], c["iters"], 0))
+    assert [psgd._powersgd._plan.fused_final(t) for t in range(2)] == [form, form], cfg

@@ -1,9 +1,12 @@
-"""One-shot all-reduce of the last factor over IPC mappings (psgd_ipc_*, PSGD_IPC_ALLREDUCE=1):
-W processes on cuda:0 (gloo for the host barriers and the earlier iterations' collectives), each
-mapping the others' exchange buffers with hipIpcOpenMemHandle and summing them in one kernel.
-Checked against the reference's own multi-worker goldens (F2), like the collective path."""
+"""One-shot all-reduce over IPC exchange buffers (psgd_aggregate_ipc, PSGD_COMM=ipc): W processes
+on cuda:0, each mapping the others' exchange buffers with hipIpcOpenMemHandle. Every factor
+all-reduce of a step (and the uncompressed tensors) is a device-side flag handshake plus a
+rank-order sum, with no host barrier or synchronisation per step (gloo carries only the one-off
+handle exchange). Checked against the reference's own multi-worker goldens (F2), like the
+collective path; plus skewed ranks and the bounded wait."""
 import os
 import tempfile
+import time
 
 import pytest
 import torch
@@ -16,8 +19,8 @@ MAN = manifest()
 TOL_FREE = 1e-4
 
 
-def _worker(rank_id, world, key, initfile):
-    os.environ["PSGD_IPC_ALLREDUCE"] = "1"
+def _worker(rank_id, world, key, initfile, skew):
+    os.environ["PSGD_COMM"] = "ipc"
     from powersgd_amd import Config, PowerSGD
 
     torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id, world_size=world)
@@ -36,6 +39,8 @@ def _worker(rank_id, world, key, initfile):
         for t in range(meta["steps"]):
             inputs = scenario_inputs(meta, t, res, rank_id)
             grads = [g.to(dev) for g in inputs]
+            if skew and rank_id == t % world:
+                time.sleep(0.3)  # this rank arrives late: the peers' kernels wait on its flags
             outs = psgd.aggregate(grads)
             torch.cuda.synchronize()
             for i, g in enumerate(inputs):
@@ -46,7 +51,8 @@ def _worker(rank_id, world, key, initfile):
                 check(er, TOL_FREE, key, rank_id, t, i, "ipc-res")
             res = [g.cpu() for g in grads]
         assert psgd._powersgd._ipc_open
-        torch.distributed.barrier()
+        assert not psgd._powersgd.ipc_status(), "a device-side exchange wait timed out"
+        psgd._powersgd.close_ipc()
     finally:
         torch.distributed.destroy_process_group()
 
@@ -55,4 +61,39 @@ def _worker(rank_id, world, key, initfile):
 def test_ipc_one_shot_allreduce_matches_reference(key):
     world = MAN["multi"][key]["world"]
     with tempfile.TemporaryDirectory() as td:
-        torch.multiprocessing.spawn(_worker, args=(world, key, os.path.join(td, "init")), nprocs=world, join=True)
+        torch.multiprocessing.spawn(_worker, args=(world, key, os.path.join(td, "init"), False), nprocs=world,
+                                    join=True)
+
+
+def test_ipc_skewed_ranks():
+    """One rank per step arrives 0.3 s late: the others' exchange kernels wait on its flag
+    (device side) and the results still match the reference goldens."""
+    key = sorted(k for k in MAN["multi"] if MAN["multi"][k]["world"] == 2)[0]
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_worker, args=(2, key, os.path.join(td, "init"), True), nprocs=2, join=True)
+
+
+def _timeout_worker(rank_id, initfile):
+    os.environ["PSGD_COMM"] = "ipc"
+    os.environ["PSGD_IPC_SPIN"] = "4000"  # ~1 ms of polling
+    from powersgd_amd import Config, PowerSGD
+
+    torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id, world_size=2)
+    try:
+        dev = torch.device("cuda:0")
+        shapes = [(64, 32), (32, 16)]
+        psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(2, 1, 2, 0))
+        psgd._powersgd._ipc_setup(0)
+        if rank_id == 0:  # rank 1 never takes the step: rank 0's waits give up, no hang
+            psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
+            torch.cuda.synchronize()
+            assert psgd._powersgd.ipc_status()
+            assert not psgd._powersgd.ipc_status()  # read-and-clear
+        psgd._powersgd.close_ipc()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_ipc_wait_is_bounded():
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_timeout_worker, args=(os.path.join(td, "init"),), nprocs=2, join=True)
