@@ -38,6 +38,10 @@
  *    RuntimeError on unsupported dtypes (:189), PSGD_ERR_LAYOUT its RuntimeError on
  *    non-viewable tensors (:289).
  *  - Not re-entrant per plan; one plan per device/process (reference: single-threaded, :146).
+ *  - Stream order: the calls of one plan must be ordered on ONE stream (as torch's current
+ *    stream orders them). The plan's device pointer tables are re-uploaded on the launch stream
+ *    when the gradient pointer set changes; a kernel of an earlier call still running on another
+ *    stream could read a slot being rewritten.
  */
 #ifndef PSGD_H
 #define PSGD_H

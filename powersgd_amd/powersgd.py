@@ -68,7 +68,12 @@ def _output_slab(shapes, code: int, dev_index: int):
     the views, handing the previous call's buffer out again only when no reference to any of
     its views survives anywhere (TensorImpl, PyObject and storage reference counts back at
     their creation values), else a fresh buffer, like the reference's per-call ``empty_like``
-    (:153). ``flat`` is the buffer of the latest call."""
+    (:153). ``flat`` is the buffer of the latest call.
+
+    Outputs are produced on the codec's stream (torch's current stream). A consumer on ANOTHER
+    stream must keep a reference to the outputs until its work is done (``record_stream`` alone
+    does not delay the reuse here, unlike torch's caching allocator): the next step writes the
+    buffer again once the last reference is dropped."""
     return _psgd_host.OutputSlab([list(s) for s in shapes], code, dev_index)
 
 

@@ -2,13 +2,15 @@
 
 usage: python tools/regs.py <source.hip> [name-substring]   (run from powersgd_amd/csrc)
 """
+import os
 import re
 import subprocess
 import sys
 
 src = sys.argv[1]
 filt = sys.argv[2] if len(sys.argv) > 2 else ""
-cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I../../include",
+EXTRA = os.environ.get("EXTRA", "").split()
+cmd = ["/opt/rocm/bin/hipcc", *EXTRA, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I../../include",
        "-x", "hip", "-c", src, "-o", "/tmp/_regs.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None

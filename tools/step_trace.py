@@ -1,0 +1,23 @@
+"""Plain world-size-1 steps of one config (no timing events, no other blocks): run under
+rocprofv3 --kernel-trace to see a step's kernel sequence and its launch gaps as the bench's
+timed loop runs them. usage: python tools/step_trace.py <config> [steps]"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from powersgd_amd import Config, PowerSGD  # noqa: E402
+from powersgd_amd.workloads import CONFIGS  # noqa: E402
+
+cfg = sys.argv[1]
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+dev = torch.device("cuda:0")
+c = CONFIGS[cfg]
+dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+gen = torch.Generator(device=dev).manual_seed(1)
+sets = [[torch.randn(s, generator=gen, device=dev).to(dtype) for s in c["shapes"]] for _ in range(4)]
+psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dtype) for s in c["shapes"]], Config(c["rank"], c["mcr"], c["iters"], 0))
+for k in range(steps):
+    psgd.aggregate(sets[k % 4])
+torch.cuda.synchronize()
+print("done")
