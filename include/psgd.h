@@ -237,7 +237,10 @@ int psgd_reconstruct(psgd_plan* plan, void* const* grads, void* const* resid_out
  * is_distributed()): for every power iteration the codec kernels and an in-place SUM all-reduce
  * of the out-factor state buffer (:204-209; the last iteration's collective grouped with the
  * SUM all-reduce of the uncompressed tensors packed /W into flat_out, utils.py:43-47), then the
- * output pass (alpha = 1/W). flat may be null (no uncompressed tensors). */
+ * output pass (alpha = 1/W). flat may be null (no uncompressed tensors). With buckets set
+ * (psgd_plan_set_buckets), the collectives run per bucket on a stream of the communicator,
+ * ordered with events: bucket b's collective overlaps bucket b+1's kernels, and bucket b of the
+ * next iteration waits only for bucket b's collective. */
 int psgd_comm_id_bytes(int64_t* bytes);
 int psgd_comm_unique_id(void* id_out);
 int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, psgd_comm** out);

@@ -16,6 +16,10 @@
 struct psgd_comm {
     ncclComm_t comm = nullptr;
     int world = 0, rank = -1, device = -1;
+    // bucketed steps (psgd_aggregate_comm with buckets): the collectives run on this stream,
+    // ordered against the codec's stream with events (kernels of bucket b+1 overlap bucket b's
+    // collective)
+    hipStream_t cs = nullptr;
 };
 
 namespace psgd {
@@ -74,6 +78,17 @@ int rccl_fail(ncclResult_t e, const char* what) {
 }  // namespace
 
 int comm_world(const psgd_comm* c) { return c->world; }
+
+hipStream_t comm_stream(psgd_comm* c) {
+    if (!c->cs) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        if (c->device >= 0) (void)hipSetDevice(c->device);
+        if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess) c->cs = nullptr;
+        if (prev >= 0 && prev != c->device) (void)hipSetDevice(prev);
+    }
+    return c->cs;
+}
 
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s) {
     const Rccl& r = rccl();
@@ -138,7 +153,9 @@ int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, 
 
 int psgd_comm_destroy(psgd_comm* c) {
     if (!c) return PSGD_OK;
+    if (c->cs) (void)hipStreamSynchronize(c->cs);
     if (c->comm) (void)rccl().destroy(c->comm);
+    if (c->cs) (void)hipStreamDestroy(c->cs);
     delete c;
     return PSGD_OK;
 }

@@ -13,6 +13,7 @@ namespace psgd {
 // two fp32 buffers, stream-ordered on s
 int comm_fail(int code, const char* msg);
 int comm_world(const psgd_comm* c);
+hipStream_t comm_stream(psgd_comm* c);  // created on first use; null if creation failed
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
 
 constexpr int kMaxTerms = 16;   // == PSGD_MAX_ITERS

@@ -441,6 +441,7 @@ struct psgd_plan {
     // benchmark timing of the final pass: event pairs recorded on the launch stream
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    std::vector<hipEvent_t> comm_ev;  // bucketed psgd_aggregate_comm: kernels-queued / collective-done
     size_t ev_used = 0;
     // one-shot IPC all-reduce (psgd_ipc_*, psgd_aggregate_ipc): this rank's exchange buffer
     // (hipMalloc'd so that it can be exported: flags header + 2 parities x iters slots), the
@@ -467,6 +468,7 @@ struct psgd_plan {
     bool qfold(int64_t step, bool agg) const { return qfold_ok && iters == 2 && proj_final(step, agg); }
 
     ~psgd_plan() {
+        for (auto& e : comm_ev) (void)hipEventDestroy(e);
         for (auto& e : ev_pool) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -2036,6 +2038,41 @@ int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t ste
         if (int st = flat_args(f, unc, flat_out, world, s, &fa)) return st;
     } else if (has_flat) {
         if (int st = psgd_flat_pack(f, unc, flat_out, world, stream)) return st;
+    }
+    const int nb = int(p->spans.size());
+    hipStream_t cs = nb > 1 ? comm_stream(comm) : nullptr;
+    if (nb > 1 && cs) {
+        // buckets of shape groups (psgd_plan_set_buckets): bucket b's collective runs on the
+        // communicator's stream as soon as bucket b's kernels are queued, under bucket b+1's
+        // kernels; bucket b of the next iteration waits only for bucket b's collective
+        if (p->comm_ev.size() < size_t(2 * nb)) {
+            for (auto& e : p->comm_ev) (void)hipEventDestroy(e);
+            p->comm_ev.assign(size_t(2 * nb), nullptr);
+            for (auto& e : p->comm_ev) PSGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        hipEvent_t* ev_k = p->comm_ev.data();       // kernels of bucket b queued on s
+        hipEvent_t* ev_c = p->comm_ev.data() + nb;  // collective of bucket b done on cs
+        for (int it = 0; it < p->iters; ++it) {
+            const bool e = p->even(step, it);
+            const bool last = it == p->iters - 1;
+            for (int b = 0; b < nb; ++b) {
+                const psgd_plan::Span& sp = p->spans[size_t(b)];
+                if (it > 0) PSGD_HIP(hipStreamWaitEvent(s, ev_c[b], 0));
+                if (int st = compress_impl(p, grads, step, it, s, false, false, (fold && b == 0) ? &fa : nullptr, &sp))
+                    return st;
+                PSGD_HIP(hipEventRecord(ev_k[b], s));
+                PSGD_HIP(hipStreamWaitEvent(cs, ev_k[b], 0));
+                float* buf = e ? p->Q + sp.q[0] : p->P + sp.p[0];
+                const size_t n = size_t(e ? sp.q[1] - sp.q[0] : sp.p[1] - sp.p[0]);
+                const bool tail = last && b == nb - 1 && has_flat;
+                if (int st = comm_allreduce(comm, buf, n, tail ? static_cast<float*>(flat_out) : nullptr,
+                                            tail ? size_t(f->total) : 0, cs))
+                    return st;
+                PSGD_HIP(hipEventRecord(ev_c[b], cs));
+            }
+        }
+        for (int b = 0; b < nb; ++b) PSGD_HIP(hipStreamWaitEvent(s, ev_c[b], 0));
+        return decompress_impl(p, grads, out, step, world, s, false);
     }
     for (int it = 0; it < p->iters; ++it) {
         if (int st = compress_impl(p, grads, step, it, s, false, false, fold ? &fa : nullptr)) return st;

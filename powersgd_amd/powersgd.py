@@ -373,6 +373,11 @@ class BasicPowerSGD(Aggregator):
                 obj = [_lib.comm_unique_id() if rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
                 self._comm = _lib.Comm(world, rank, obj[0], self._dev_index)
+                # PSGD_COMM_BUCKETS > 1: the library overlaps bucket b's collective (its own
+                # stream) with bucket b+1's kernels (psgd_aggregate_comm)
+                nb = int(os.environ.get("PSGD_COMM_BUCKETS", "1"))
+                if nb > 1 and self._buckets is None:
+                    self._setup_buckets(nb)
         return self._comm or None
 
     def _attach_tail(self, numel: int) -> None:
@@ -437,14 +442,15 @@ class BasicPowerSGD(Aggregator):
         self.step_counter += 1
         return outs
 
-    def _setup_buckets(self) -> None:
+    def _setup_buckets(self, want: Optional[int] = None) -> None:
         """Cut the shape groups into up to PSGD_BUCKETS (default 4) consecutive buckets of about
         equal gradient size. Each iteration's factor all-reduce (reference :204-209) is then
         issued per bucket slice, asynchronously, right after that bucket's kernels: bucket b's
         collective overlaps bucket b+1's product (RCCL runs on its own stream), and the next
         iteration of bucket b waits only for bucket b's collective. SUM over slices == SUM over
         the whole buffer, element by element. fp64 plans and PSGD_BUCKETS=1 keep one collective."""
-        want = int(os.environ.get("PSGD_BUCKETS", "4"))
+        if want is None:
+            want = int(os.environ.get("PSGD_BUCKETS", "4"))
         groups = self._plan.groups()
         if self.dtype == torch.float64 or want <= 1 or len(groups) < 2:
             self._buckets = [(0, self._ps_buffer.numel(), 0, self._qs_buffer.numel())]
