@@ -229,6 +229,9 @@ def main():
         # the same step with every factor all-reduce as a one-shot sum over IPC exchange buffers
         # (device-side flags, no collective library): beside the RCCL headline, not instead of it
         out["ipc_exchange"] = ipc_block(a, world, rank, dev, backend)
+    if world > 1 and backend == "nccl" and "PSGD_COMM_BUCKETS" not in os.environ:
+        # the RCCL step with 2 buckets: each bucket's collective under the next bucket's kernels
+        out["rccl_buckets2"] = env_block(a, world, rank, dev, backend, {"PSGD_COMM_BUCKETS": "2"})
     if rank == 0 and world == 1 and not a.no_extra:
         # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
         # world size 1, cold, same steps
@@ -274,6 +277,24 @@ def ipc_block(a, world, rank, dev, backend):
         del os.environ["PSGD_COMM"]
 
 
+def env_block(a, world, rank, dev, backend, env):
+    """The headline workload again under extra environment knobs (read at plan creation)."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        m = measure(a, a.config, world, rank, dev, backend, "cold", dist_path=True)
+        blk = {k: m[k] for k in ("value", "ms_per_step", "step_roofline")}
+        blk["env"] = env
+        blk["buckets"] = m["config"]["buckets"]
+        return blk
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
 def one_rank_group(a, dev):
     """cfg3 and cfg2 through PowerSGD.aggregate with torch.distributed initialised as ONE RCCL
     rank on this GPU: is_distributed() is True, so the exact multi-GPU code path runs."""
@@ -291,6 +312,14 @@ def one_rank_group(a, dev):
             m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
             res[cfg] = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
             res[cfg]["buckets"] = m["config"]["buckets"]
+        # the bucketed overlap's launch cost with nothing to hide (one rank: no xGMI traffic)
+        os.environ["PSGD_COMM_BUCKETS"] = "2"
+        try:
+            m = measure(a, "cfg2_resnet50_r1", 1, 0, dev, "nccl", "cold", dist_path=True)
+            res["rccl_buckets2"] = {"cfg2_resnet50_r1": {"ms_per_step": m["ms_per_step"], "value": m["value"],
+                                                         "buckets": m["config"]["buckets"]}}
+        finally:
+            del os.environ["PSGD_COMM_BUCKETS"]
         # the IPC exchange path (psgd_aggregate_ipc) of the same configs: its flag handshake and
         # rank-order sums with W = 1 (own buffer only)
         os.environ["PSGD_COMM"] = "ipc"

@@ -19,7 +19,8 @@ def _rel(a, b, scale):
     return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
 
 
-def _worker(_, port, cfg, steps):
+def _worker(_, port, cfg, steps, buckets=1):
+    os.environ["PSGD_COMM_BUCKETS"] = str(buckets)
     from oracle import powersgd_oracle as O
     from powersgd_amd import Config, PowerSGD, _lib
     from powersgd_amd.workloads import CONFIGS, hash_tensors
@@ -46,6 +47,8 @@ def _worker(_, port, cfg, steps):
             oc = O.policy_step(ora, gc)
             torch.cuda.synchronize()
             assert isinstance(psgd._powersgd._comm, _lib.Comm)  # the library's RCCL path ran
+            if buckets > 1:  # the bucketed overlap (collectives on the communicator's stream)
+                assert psgd._powersgd._buckets is not None and len(psgd._powersgd._buckets) > 1
             for i, g in enumerate(scale):
                 tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
                 check(_rel(od[i], oc[i], g), tol, cfg, t, i, "out")
@@ -61,3 +64,13 @@ def test_rccl_step_one_rank_vs_oracle(cfg):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     torch.multiprocessing.spawn(_worker, args=(port, cfg, 3), nprocs=1, join=True)
+
+
+@pytest.mark.parametrize("cfg", ["cfg3_resnet50_r4", "cfg2_resnet50_r1"])
+def test_rccl_bucketed_overlap_vs_oracle(cfg):
+    """PSGD_COMM_BUCKETS=4: per-bucket kernels on the codec's stream, per-bucket collectives on
+    the communicator's stream, ordered by events: same results as the single collective."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    torch.multiprocessing.spawn(_worker, args=(port, cfg, 3, 4), nprocs=1, join=True)
