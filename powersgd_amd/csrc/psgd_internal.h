@@ -343,6 +343,14 @@ struct XchgArgs {
     uint32_t spin_limit;       // polls (~0.25 us apart) before a wait gives up
     int32_t world, rank;
     int32_t* err;              // set to 1 when a wait timed out (psgd_ipc_status)
+    // rank-1 norm fold (non-last iterations): one workgroup per reduction item of this parity
+    // (items, nitems, mats, even) writes the sum to dst and dst2 (the raw copy the next
+    // iteration's kernels normalise on the fly) and the item's sum of squares to ss_out
+    const RedItem* items;
+    const MatDesc* mats;
+    float* dst2;
+    float* ss_out;
+    int32_t nitems, even;
 };
 hipError_t launch_xchg(const XchgArgs& a, hipStream_t s);
 

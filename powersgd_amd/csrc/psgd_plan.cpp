@@ -452,6 +452,9 @@ struct psgd_plan {
     int64_t ipc_slot = 0, ipc_flat_off = 0, ipc_flat_cap = 0;
     size_t o_ipc_ptrs = 0, o_xerr = 0;
     float* xout_now = nullptr;  // set per iteration by psgd_aggregate_ipc (exchange slot)
+    // history slot of the RAW in-factor the rank-1 norm fold reads: 1 (the local reduction's
+    // output, world size 1) or 2 (the exchange's summed copy, psgd_aggregate_ipc)
+    int raw_slot = 1;
     int64_t xslot_off(int64_t step, int it) const {  // byte offset of a slot in every buffer
         return kXchgHeader + ((step & 1) * iters + it) * ipc_slot * int64_t(sizeof(float));
     }
@@ -1422,7 +1425,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
         fa.grads = p->grad_tab.table();
         fa.out = p->out_now;
-        fa.x = fused ? p->hist(1, it - 1) : p->hist(0, it);
+        fa.x = fused ? p->hist(p->raw_slot, it - 1) : p->hist(0, it);
         fill_terms(p, step, it, fa.res);
         fa.nres = it;
         fa.write_out = write_out ? 1 : 0;
@@ -1456,7 +1459,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     ProductArgs pa{};
     pa.mats = p->dev<MatDesc>(p->o_mats);
     pa.grads = p->grad_tab.table();
-    pa.x = fused ? p->hist(1, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
+    pa.x = fused ? p->hist(p->raw_slot, it - 1) : fused0 ? in : p->hist(0, it);  // fused: the raw factor
     pa.part = p->dev<float>(p->o_part);
     if (fused0) pa.ss0 = p->dev<float>(p->o_ss0);
     fill_terms(p, step, it, pa.res);
@@ -1505,7 +1508,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         ra.grng_in = prev_grng;
         ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even) + rn[0];
         ra.nnorm = rn[1] - rn[0];
-        ra.raw = p->hist(1, it - 1);
+        ra.raw = p->hist(p->raw_slot, it - 1);
         ra.xstate = in;
         ra.hx = p->hist(0, it);
     }
@@ -2120,13 +2123,27 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
         if (int st = flat_args(f, unc, flat_slot, world, s, &fa)) return st;
         if (!fold) PSGD_HIP(launch_flat_pack(f->dtype, fa, s));
     }
+    // rank 1: the joint group norm of every summed factor is folded as at world size 1 (no
+    // k_orth_reg launch): k_xchg leaves per-item sums of squares and a raw copy (history slot 2)
+    // that the next iteration's kernels normalise on the fly
+    const bool nfold = p->rbucket == 1 && env_int("PSGD_IPC_NORM_FOLD", 1) != 0;
     for (int it = 0; it < p->iters; ++it) {
         p->xout_now = p->xslot(step, it);
-        const int st = compress_impl(p, grads, step, it, s, false, false, fold ? &fa : nullptr);
+        p->raw_slot = 2;
+        const int st = compress_impl(p, grads, step, it, s, nfold, false, fold ? &fa : nullptr);
         p->xout_now = nullptr;
+        p->raw_slot = 1;
         if (st) return st;
         const bool e = p->even(step, it);
         XchgArgs xa{};
+        if (nfold && it + 1 < p->iters) {
+            xa.items = p->dev<RedItem>(e ? p->o_red_even : p->o_red_odd);
+            xa.nitems = int32_t(e ? p->red_even.size() : p->red_odd.size());
+            xa.mats = p->dev<MatDesc>(p->o_mats);
+            xa.even = e ? 1 : 0;
+            xa.dst2 = p->hist(2, it);
+            xa.ss_out = p->dev<float>(p->o_ss) + size_t(it & 1) * p->ss_stride;
+        }
         xa.peers = p->dev<const char* const>(p->o_ipc_ptrs);
         xa.own_flag = reinterpret_cast<uint64_t*>(p->ipc_buf) + it;
         xa.flag_off = int64_t(it) * int64_t(sizeof(uint64_t));

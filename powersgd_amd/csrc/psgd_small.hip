@@ -1948,6 +1948,29 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
     }
     __syncthreads();
+    if (a.items) {  // one reduction item per workgroup (<= 256 consecutive factor elements)
+        __shared__ float wsq[kWaves];
+        const RedItem it = a.items[blockIdx.x];
+        const MatDesc d = a.mats[it.mat];
+        const int64_t e = (a.even ? d.qoff : d.poff) + it.start + tid;
+        float sq = 0.f;
+        if (tid < it.cnt) {
+            float s = 0.f;
+            for (int w = 0; w < a.world; ++w) {
+                const float* p = reinterpret_cast<const float*>(a.peers[w] + a.slot_off) + e;
+                const float v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                s = w == 0 ? v : s + v;  // rank order
+            }
+            a.dst[e] = s;
+            a.dst2[e] = s;
+            sq = s * s;
+        }
+        sq = wave_allsum(sq);
+        if ((tid & 63) == 0) wsq[tid >> 6] = sq;
+        __syncthreads();
+        if (tid == 0) a.ss_out[blockIdx.x] = ((wsq[0] + wsq[1]) + wsq[2]) + wsq[3];
+        return;
+    }
     // quads of the factor, then quads of the flat region; buffer bounds zero-fill a ragged tail
     const int64_t qf = (a.n + 3) / 4, qt = qf + (a.nflat + 3) / 4;
     const int64_t stride = int64_t(gridDim.x) * kBlock;
@@ -1967,6 +1990,10 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
 }
 
 hipError_t launch_xchg(const XchgArgs& a, hipStream_t s) {
+    if (a.items) {
+        k_xchg<<<a.nitems < 1 ? 1 : a.nitems, kBlock, 0, s>>>(a);
+        return hipGetLastError();
+    }
     const int64_t quads = (a.n + 3) / 4 + (a.nflat + 3) / 4;
     const int64_t blocks = (quads + kBlock - 1) / kBlock;
     // at least one workgroup (it raises the flag), at most one per CU

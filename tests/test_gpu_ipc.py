@@ -97,3 +97,49 @@ def _timeout_worker(rank_id, initfile):
 def test_ipc_wait_is_bounded():
     with tempfile.TemporaryDirectory() as td:
         torch.multiprocessing.spawn(_timeout_worker, args=(os.path.join(td, "init"),), nprocs=2, join=True)
+
+
+def _one_rank_worker(_, initfile, cfg, steps):
+    """The IPC exchange path with one rank (own buffer only) against the CPU oracle per step:
+    the BASELINE shapes, incl. four power iterations (the rank-1 norm fold of every iteration)."""
+    os.environ["PSGD_COMM"] = "ipc"
+    from oracle import powersgd_oracle as O
+    from powersgd_amd import Config, PowerSGD
+    from powersgd_amd.workloads import CONFIGS, hash_tensors
+
+    torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=0, world_size=1)
+    try:
+        dev = torch.device("cuda:0")
+        c = CONFIGS[cfg]
+        shapes = c["shapes"]
+        psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+        ora = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
+        ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
+        ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+        res_d = [torch.zeros(s, device=dev) for s in shapes]
+        res_c = [torch.zeros(s) for s in shapes]
+        for t in range(steps):
+            new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=700 + t)]
+            gd = [r + x.to(dev) for r, x in zip(res_d, new)]
+            gc = [r + x for r, x in zip(res_c, new)]
+            scale = [g.clone() for g in gc]
+            od = psgd.aggregate(gd)
+            oc = O.policy_step(ora, gc)
+            torch.cuda.synchronize()
+            for i, g in enumerate(scale):
+                tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
+                eo = float((od[i].cpu().double() - oc[i].double()).norm()) / max(float(g.norm()), 1e-30)
+                er = float((gd[i].cpu().double() - gc[i].double()).norm()) / max(float(g.norm()), 1e-30)
+                check(eo, tol, cfg, 0, t, i, "ipc1-out")
+                check(er, tol, cfg, 0, t, i, "ipc1-res")
+            res_d, res_c = gd, gc
+        assert not psgd._powersgd.ipc_status()
+        psgd._powersgd.close_ipc()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", ["cfg2_resnet50_r1", "cfg5_lstm_r1_i4", "cfg3_resnet50_r4"])
+def test_ipc_one_rank_vs_oracle(cfg):
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_one_rank_worker, args=(os.path.join(td, "init"), cfg, 3), nprocs=1, join=True)
