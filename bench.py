@@ -183,6 +183,8 @@ def timed(fn, steps, world, dev):
 
 def main():
     a = parse()
+    # bounded device-side waits of the IPC exchange blocks: ~1 s per wait (default ~18 s)
+    os.environ.setdefault("PSGD_IPC_SPIN", str(1 << 22))
     env_world = os.environ.get("WORLD_SIZE")
     if a.gpus > 1 and env_world is None:
         sys.exit(launch_ranks(a))
@@ -359,6 +361,19 @@ def measure(a, cfg_name, world, rank, dev, backend, mode, dist_path=False):
     for k in range(a.warmup):
         psgd.aggregate(sets[k % S])
     torch.cuda.synchronize()
+    if codec._ipc_open:
+        # the IPC exchange's device-side waits are bounded (PSGD_IPC_SPIN, ~1 s here): if any
+        # rank's warm-up wait gave up, every rank abandons the block instead of timing garbage
+        bad = [None] * world
+        mine = codec.ipc_status()
+        if world > 1:
+            torch.distributed.all_gather_object(bad, mine)
+        else:
+            bad = [mine]
+        if any(bad):
+            codec.close_ipc()
+            raise RuntimeError(f"IPC exchange wait timed out during warm-up on rank(s) "
+                               f"{[r for r, b in enumerate(bad) if b]}")
 
     # timed regions: K plain steps each (no instrumentation inside); cold = rotating sets
     do_cold, do_warm = mode in ("both", "cold"), mode in ("both", "warm")

@@ -351,6 +351,10 @@ struct XchgArgs {
     float* dst2;
     float* ss_out;
     int32_t nitems, even;
+    // ranks 2/4, two iterations: the upper Gram of each item's rows of the SUMMED Q (fp64,
+    // kGramStride per item) for k_orth_chain, as k_reduce leaves it at world size 1
+    double* gram;
+    int32_t gram_r;
 };
 hipError_t launch_xchg(const XchgArgs& a, hipStream_t s);
 

@@ -455,6 +455,9 @@ struct psgd_plan {
     // history slot of the RAW in-factor the rank-1 norm fold reads: 1 (the local reduction's
     // output, world size 1) or 2 (the exchange's summed copy, psgd_aggregate_ipc)
     int raw_slot = 1;
+    // psgd_aggregate_ipc, ranks 2/4, two iterations: the exchange of iteration 0 left the summed
+    // Q panels' Gram partials, so iteration 1 orthonormalises with k_orth_chain
+    bool xgram_now = false;
     int64_t xslot_off(int64_t step, int it) const {  // byte offset of a slot in every buffer
         return kXchgHeader + ((step & 1) * iters + it) * ipc_slot * int64_t(sizeof(float));
     }
@@ -1390,14 +1393,17 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     // partials and k_orth_chain (no Gram pass, panel rows over several workgroups) replaces
     // k_orth_chol
     const bool qf = p->qfold(step, write_out);
+    const bool xg = p->xgram_now && it == 1 && !even;  // the exchange left the summed Q's Gram
     float* ss = p->dev<float>(p->o_ss);
 
-    if (qf && proj) {
+    if ((qf && proj) || xg) {
         ChainArgs ca{};
         ca.units = p->dev<OrthUnit>(p->o_units_q) + sp.uq[0];
         ca.uitems = p->dev<int32_t>(p->o_uitems) + 2 * sp.uq[0];
         ca.gram = p->dev<double>(p->o_gram);
-        ca.raw = p->hist(1, it - 1);  // the even iteration's reduced Q (k_reduce's yloc)
+        // the even iteration's reduced Q: k_reduce's yloc (world size 1) or the exchange's
+        // summed copy (history slot 2, psgd_aggregate_ipc)
+        ca.raw = xg ? p->hist(2, it - 1) : p->hist(1, it - 1);
         ca.state = in;
         ca.hx = p->hist(0, it);
         ca.rfac = p->dev<float>(p->o_rq);
@@ -2127,12 +2133,17 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
     // k_orth_reg launch): k_xchg leaves per-item sums of squares and a raw copy (history slot 2)
     // that the next iteration's kernels normalise on the fly
     const bool nfold = p->rbucket == 1 && env_int("PSGD_IPC_NORM_FOLD", 1) != 0;
+    // ranks 2/4, two iterations (every step starts even): the Q orthonormalisation from the
+    // exchange's Gram partials of the summed Q (k_orth_chain instead of k_orth_chol)
+    const bool gfold = p->qfold_ok && p->iters == 2 && p->even(step, 0) && env_int("PSGD_IPC_GRAM_FOLD", 1) != 0;
     for (int it = 0; it < p->iters; ++it) {
         p->xout_now = p->xslot(step, it);
         p->raw_slot = 2;
+        p->xgram_now = gfold;
         const int st = compress_impl(p, grads, step, it, s, nfold, false, fold ? &fa : nullptr);
         p->xout_now = nullptr;
         p->raw_slot = 1;
+        p->xgram_now = false;
         if (st) return st;
         const bool e = p->even(step, it);
         XchgArgs xa{};
@@ -2143,6 +2154,15 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
             xa.even = e ? 1 : 0;
             xa.dst2 = p->hist(2, it);
             xa.ss_out = p->dev<float>(p->o_ss) + size_t(it & 1) * p->ss_stride;
+        }
+        if (gfold && it == 0) {  // even: the Q side; k_orth_chain of iteration 1 reads the Gram
+            xa.items = p->dev<RedItem>(p->o_red_even);
+            xa.nitems = int32_t(p->red_even.size());
+            xa.mats = p->dev<MatDesc>(p->o_mats);
+            xa.even = 1;
+            xa.dst2 = p->hist(2, it);
+            xa.gram = p->dev<double>(p->o_gram);
+            xa.gram_r = p->rbucket;
         }
         xa.peers = p->dev<const char* const>(p->o_ipc_ptrs);
         xa.own_flag = reinterpret_cast<uint64_t*>(p->ipc_buf) + it;

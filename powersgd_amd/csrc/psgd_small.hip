@@ -1950,12 +1950,12 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
     __syncthreads();
     if (a.items) {  // one reduction item per workgroup (<= 256 consecutive factor elements)
         __shared__ float wsq[kWaves];
+        __shared__ float xv[kRedItem];
         const RedItem it = a.items[blockIdx.x];
         const MatDesc d = a.mats[it.mat];
         const int64_t e = (a.even ? d.qoff : d.poff) + it.start + tid;
-        float sq = 0.f;
+        float sq = 0.f, s = 0.f;
         if (tid < it.cnt) {
-            float s = 0.f;
             for (int w = 0; w < a.world; ++w) {
                 const float* p = reinterpret_cast<const float*>(a.peers[w] + a.slot_off) + e;
                 const float v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1965,10 +1965,42 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
             a.dst2[e] = s;
             sq = s * s;
         }
-        sq = wave_allsum(sq);
-        if ((tid & 63) == 0) wsq[tid >> 6] = sq;
-        __syncthreads();
-        if (tid == 0) a.ss_out[blockIdx.x] = ((wsq[0] + wsq[1]) + wsq[2]) + wsq[3];
+        if (a.ss_out) {
+            sq = wave_allsum(sq);
+            if ((tid & 63) == 0) wsq[tid >> 6] = sq;
+            __syncthreads();
+            if (tid == 0) a.ss_out[blockIdx.x] = ((wsq[0] + wsq[1]) + wsq[2]) + wsq[3];
+        }
+        if (a.gram) {
+            // the item's rows (it starts on a row and holds whole rows of r elements): lane l
+            // of wave 0 takes rows l, l + 64, ...; fp64 products, one wave tree per entry
+            xv[tid] = s;
+            __syncthreads();
+            if (tid >= 64) return;
+            const int r = a.gram_r, nrow = it.cnt / r;
+            double g[kGramStride];
+#pragma unroll
+            for (int k = 0; k < kGramStride; ++k) g[k] = 0.0;
+            for (int row = tid; row < nrow; row += 64) {
+                int k = 0;
+                for (int c = 0; c < r; ++c)
+                    for (int b = c; b < r; ++b) {
+                        const double prod = double(xv[row * r + c]) * double(xv[row * r + b]);
+#pragma unroll
+                        for (int q = 0; q < kGramStride; ++q)
+                            if (q == k) g[q] += prod;
+                        ++k;
+                    }
+            }
+            const int ng = r * (r + 1) / 2;
+#pragma unroll
+            for (int k = 0; k < kGramStride; ++k) {
+                if (k < ng) {
+                    const double t = wave_allsum_f64(g[k]);
+                    if (tid == 0) a.gram[int64_t(blockIdx.x) * kGramStride + k] = t;
+                }
+            }
+        }
         return;
     }
     // quads of the factor, then quads of the flat region; buffer bounds zero-fill a ragged tail
