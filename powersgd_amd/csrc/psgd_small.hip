@@ -1956,10 +1956,17 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
         const int64_t e = (a.even ? d.qoff : d.poff) + it.start + tid;
         float sq = 0.f, s = 0.f;
         if (tid < it.cnt) {
-            for (int w = 0; w < a.world; ++w) {
-                const float* p = reinterpret_cast<const float*>(a.peers[w] + a.slot_off) + e;
-                const float v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                s = w == 0 ? v : s + v;  // rank order
+            for (int w0 = 0; w0 < a.world; w0 += kXchgUnroll) {  // the peers' loads in flight together
+                float v[kXchgUnroll];
+#pragma unroll
+                for (int u = 0; u < kXchgUnroll; ++u)  // uniform guard: no load past the last peer
+                    v[u] = w0 + u < a.world
+                               ? __hip_atomic_load(reinterpret_cast<const float*>(a.peers[w0 + u] + a.slot_off) + e,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                               : 0.f;
+#pragma unroll
+                for (int u = 0; u < kXchgUnroll; ++u)
+                    if (w0 + u < a.world) s = w0 + u == 0 ? v[u] : s + v[u];  // rank order
             }
             a.dst[e] = s;
             a.dst2[e] = s;
