@@ -24,11 +24,12 @@
 namespace psgd {
 
 // Rows per row group per batch (each batch double-buffered: the next batch's loads are in
-// flight while this one reduces and stores): 2, or 1 at rank 4. Workgroup size: 512
+// flight while this one reduces and stores): 1 (ranks 1/2: 2 measured 0.6-2 us slower on the
+// ResNet-50 and Llama final passes, profiles/r03/v, profiles/r03/x; fewer registers per row). Workgroup size: 512
 // threads at rank 4 (a row spread over twice the threads keeps the per-thread factor
 // panels, S * 4 * r floats each, within two waves per SIMD), else 256.
 #ifndef PSGD_FIN_RB12
-#define PSGD_FIN_RB12 2
+#define PSGD_FIN_RB12 1
 #endif
 template <int R>
 struct FinRB {

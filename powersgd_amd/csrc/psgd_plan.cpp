@@ -151,7 +151,7 @@ struct FinGeom {
 // Fused final odd pass (psgd_final.cuh): row groups of T threads (4 columns each, S
 // segments), fin_rb(R) rows per group per batch, blocks of about fin_elems elements.
 #ifndef PSGD_FIN_RB12
-#define PSGD_FIN_RB12 2
+#define PSGD_FIN_RB12 1
 #endif
 int fin_rb(int R) { return R == 4 ? 1 : PSGD_FIN_RB12; }   // == FinRB<R>
 int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
