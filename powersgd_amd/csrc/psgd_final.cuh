@@ -521,9 +521,9 @@ hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* wa
     }
     if (ntiles == 0) return hipSuccess;
     if constexpr (PJ)
-        k_final_proj<T, R, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
+        timed_launch(&k_final_proj<T, R, SMAX>, dim3(ntiles + a.flat.nitems), dim3(NT), s, a);
     else
-        k_final_odd<T, R, K, SMAX><<<dim3(ntiles + a.flat.nitems), dim3(NT), 0, s>>>(a);
+        timed_launch(&k_final_odd<T, R, K, SMAX>, dim3(ntiles + a.flat.nitems), dim3(NT), s, a);
     return hipGetLastError();
 }
 

@@ -16,6 +16,14 @@ int comm_world(const psgd_comm* c);
 hipStream_t comm_stream(psgd_comm* c);  // created on first use; null if creation failed
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
 
+// Benchmark timing of the final pass (psgd_plan_set_timing): while set, the final-pass launch
+// records these events from its own dispatch packet (hipExtLaunchKernel), so the measured span
+// is the kernel alone, without the marker packets of separate hipEventRecord calls.
+struct KernelTiming {
+    hipEvent_t start, stop;
+};
+extern thread_local const KernelTiming* g_kernel_timing;
+
 constexpr int kMaxTerms = 16;   // == PSGD_MAX_ITERS
 constexpr int kBlock = 256;     // threads per workgroup for the streaming kernels
 constexpr int kWaves = kBlock / 64;

@@ -301,6 +301,7 @@ struct DevScope {  // make `dev` current for the scope, restore afterwards
 
 namespace psgd {
 int comm_fail(int code, const char* msg) { return fail(code, msg); }
+thread_local const KernelTiming* g_kernel_timing = nullptr;
 }  // namespace psgd
 
 // Persistent even product (k_even): workgroups per launch (CUs x workgroups per CU), at least
@@ -1283,9 +1284,24 @@ static bool norm0_fold() {
     return on;
 }
 
-// Timing (benchmarks): HIP events around the final pass (k_apply, or the fused final odd
-// kernel), recorded on the launch stream.
+// Timing (benchmarks): HIP events of the final pass (k_apply, or the fused final odd kernel):
+// recorded by the kernel's own dispatch (timed_launch) for the fp32/bf16 kernels, or around the
+// launch on its stream (fp64 apply).
+struct TimedScope {
+    KernelTiming kt{};
+    explicit TimedScope(const std::pair<hipEvent_t, hipEvent_t>* ev) {
+        if (ev) {
+            kt = KernelTiming{ev->first, ev->second};
+            g_kernel_timing = &kt;
+        }
+    }
+    ~TimedScope() { g_kernel_timing = nullptr; }
+};
+static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEvent_t>** ev, bool direct);
 static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEvent_t>** ev) {
+    return timing_begin(p, s, ev, false);
+}
+static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEvent_t>** ev, bool direct) {
     *ev = nullptr;
     if (!p->timing) return PSGD_OK;
     if (p->ev_used == p->ev_pool.size()) {
@@ -1297,7 +1313,7 @@ static int timing_begin(psgd_plan* p, hipStream_t s, std::pair<hipEvent_t, hipEv
         p->ev_pool.push_back(e);
     }
     *ev = &p->ev_pool[p->ev_used++];
-    PSGD_HIP(hipEventRecord((*ev)->first, s));
+    if (!direct) PSGD_HIP(hipEventRecord((*ev)->first, s));
     return PSGD_OK;
 }
 
@@ -1456,9 +1472,9 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         if (fl && write_out) fa.flat = *fl;  // uncompressed tensors ride in the same launch
         if (nfin + fa.flat.nitems == 0) return PSGD_OK;
         std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-        if (int st = timing_begin(p, s, &ev)) return st;  // benchmark timing: the final pass
+        if (int st = timing_begin(p, s, &ev, true)) return st;  // benchmark timing: the final pass
+        TimedScope ts(ev);
         PSGD_HIP(launch_final_odd(p->dtype, p->rbucket, fa.nres, fin_bucket(p->fin_smax), fa, nfin, s));
-        if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
         return PSGD_OK;
     }
 
@@ -1572,9 +1588,9 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     if (fl) aa.flat = *fl;  // uncompressed tensors ride in the same launch
     if (nt + aa.flat.nitems == 0) return PSGD_OK;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
-    if (int st = timing_begin(p, s, &ev)) return st;
+    if (int st = timing_begin(p, s, &ev, true)) return st;
+    TimedScope ts(ev);
     PSGD_HIP(launch_apply(p->dtype, p->rbucket, I, world == 1, aa, nt, s));
-    if (ev) PSGD_HIP(hipEventRecord(ev->second, s));
     return PSGD_OK;
 }
 

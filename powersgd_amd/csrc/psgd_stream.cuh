@@ -26,6 +26,7 @@
 #pragma once
 
 #include <hip/hip_bf16.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "psgd_internal.h"
@@ -69,6 +70,15 @@ __device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
 #ifndef PSGD_ST_AUX
 #define PSGD_ST_AUX 19
 #endif
+// A kernel launch that honours g_kernel_timing (psgd_internal.h)
+template <typename... Args>
+inline void timed_launch(void (*k)(Args...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    if (g_kernel_timing)
+        hipExtLaunchKernelGGL(k, grid, block, 0, s, g_kernel_timing->start, g_kernel_timing->stop, 0, args...);
+    else
+        hipLaunchKernelGGL(k, grid, block, 0, s, args...);
+}
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t kOob = 0x80000000u;  // beyond every descriptor (num_records < 2^31)
 
@@ -1062,9 +1072,9 @@ hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int nti
 #define PSGD_A(NN)                                                                       \
     do {                                                                                 \
         if (shared)                                                                      \
-            k_apply<T, R, NN, true><<<grid, block, 0, s>>>(a);                           \
+            timed_launch(&k_apply<T, R, NN, true>, grid, block, s, a);                   \
         else                                                                             \
-            k_apply<T, R, NN, false><<<grid, block, 0, s>>>(a);                          \
+            timed_launch(&k_apply<T, R, NN, false>, grid, block, s, a);                  \
     } while (0)
     if constexpr (kCache && kMaxNI == 4) {
         switch (NI) {
