@@ -1906,6 +1906,9 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
 // that never arrives sets a.err instead of hanging the queue) and sums its share of the W slots
 // in rank order, so every rank computes bitwise the same values. Peer data is read with
 // system-scope loads: no stale line a previous step left in this XCD's caches can be hit.
+#ifndef PSGD_XCHG_FLAG_ORDER
+#define PSGD_XCHG_FLAG_ORDER __ATOMIC_RELAXED
+#endif
 // System-scope (sc0 | sc1) 16-byte loads: they miss in every non-coherent cache level.
 constexpr int kSysAux = 17;
 constexpr int kXchgUnroll = 8;  // peers whose loads are in flight together
@@ -1933,8 +1936,12 @@ __device__ __forceinline__ void xchg_sum_quad(const XchgArgs& a, int64_t src_byt
 
 __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
     const int tid = threadIdx.x;
+    // the slot data were written by the PREVIOUS kernels of this stream: their completion
+    // (kernel-end release, at least agent scope: the L2s written back) already made them visible
+    // to every reader of this GPU's memory, so the flag needs no fence of its own (a release here
+    // would write this XCD's L2 back again), only a store that goes to memory (system scope)
     if (blockIdx.x == 0 && tid == 0)
-        __hip_atomic_store(a.own_flag, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.own_flag, a.epoch, PSGD_XCHG_FLAG_ORDER, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid < a.world && tid != a.rank) {  // lane w polls peer w: the W round trips overlap
         const uint64_t* f = reinterpret_cast<const uint64_t*>(a.peers[tid] + a.flag_off);
         uint32_t spins = 0;
