@@ -29,8 +29,8 @@ class Model(torch.nn.Module):
         g = torch.Generator(device=dev).manual_seed(5)
         self.xs = [torch.randn(s, generator=g, device=dev) for s in shapes]
 
-    def forward(self):
-        return sum((p * x).sum() for p, x in zip(self.ps, self.xs))
+    def forward(self, z):  # z: a dummy input (DDP's forward needs one)
+        return sum((p * x).sum() for p, x in zip(self.ps, self.xs)) + z.sum()
 
 
 def timed(fn, steps):
@@ -56,6 +56,7 @@ def main():
     torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                          device_id=dev)
     conf = Config(c["rank"], c["mcr"], c["iters"], 0)
+    z = torch.zeros(1, device=dev)
     res = {"workload": cfg, "steps": steps, "note": "1-rank RCCL group on one GPU; ms per training iteration"}
     try:
         m = Model(c["shapes"], dev)
@@ -64,7 +65,7 @@ def main():
 
         def it_ddp():
             opt.zero_grad(set_to_none=True)
-            ddp().backward()
+            ddp(z).backward()
             opt.step()
         res["ddp_allreduce"] = round(timed(it_ddp, steps), 4)
 
@@ -76,7 +77,7 @@ def main():
 
         def it_hook():
             opt2.zero_grad(set_to_none=True)
-            ddp2().backward()
+            ddp2(z).backward()
             opt2.step()
         res["ddp_powersgd"] = round(timed(it_hook, steps), 4)
 
@@ -85,7 +86,7 @@ def main():
         agg = PowerSGD(list(m3.parameters()), conf)
 
         def it_ref():
-            m3().backward()  # p.grad holds the residual: backward adds onto it (reference README)
+            m3(z).backward()  # p.grad holds the residual: backward adds onto it (reference README)
             optimizer_step(opt3, agg)
         res["optimizer_step"] = round(timed(it_ref, steps), 4)
 
