@@ -51,10 +51,13 @@ class PowerSGDState:
         p0 = self.params[0]
         self.residual = torch.zeros(numel, dtype=p0.dtype, device=p0.device)
         self.views: List[torch.Tensor] = []
+        self._offs: List[int] = []
         off = 0
         for p in self.params:
+            self._offs.append(off)
             self.views.append(self.residual[off:off + p.numel()].view(p.shape))
             off += p.numel()
+        self._gidx: Dict[tuple, torch.Tensor] = {}
         self.powersgd = PowerSGD(self.views, config)
         self._seen = [False] * len(self.params)
         self._nseen = 0
@@ -72,11 +75,15 @@ class PowerSGDState:
                 if self._seen[i]:
                     raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
                 idx.append(i)
-            for g, i in zip(grads, idx):
-                self.views[i].add_(g)  # error feedback: residual + fresh gradient
+            buf = bucket.buffer()
+            gidx = self._gather_index(buf, grads, idx)
+            # error feedback: residual + fresh gradient, the whole bucket in one indexed add
+            # (bucket buffer position -> residual position; every position once)
+            self.residual.index_add_(0, gidx, buf)
+            for i in idx:
                 self._seen[i] = True
                 self._nseen += 1
-            self._pending.append((bucket.buffer(), grads, idx, fut))
+            self._pending.append((buf, gidx, fut))
             if self._nseen == len(self.params):
                 self._complete()
             elif bucket.is_last():
@@ -103,17 +110,27 @@ class PowerSGDState:
         if not fut.done():
             fut.set_exception(err)
 
+    def _gather_index(self, buf: torch.Tensor, grads, idx) -> torch.Tensor:
+        """Device index: position k of the bucket's flat buffer -> its position in the state's
+        flat residual (built once per bucket layout; DDP rebuilds its buckets once)."""
+        key = (buf.numel(), tuple(idx), tuple((g.data_ptr() - buf.data_ptr()) // buf.element_size() for g in grads))
+        gidx = self._gidx.get(key)
+        if gidx is None:
+            host = torch.empty(buf.numel(), dtype=torch.long)
+            for g, i in zip(grads, idx):
+                off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
+                host[off:off + g.numel()] = torch.arange(self._offs[i], self._offs[i] + g.numel())
+            gidx = self._gidx[key] = host.to(buf.device)
+        return gidx
+
     def _complete(self) -> None:
         outs = self.powersgd.aggregate(self.views)  # leaves the new residual in self.views
         pending, self._pending = self._pending, []
         self._seen = [False] * len(self.params)
         self._nseen = 0
-        for buf, grads, idx, fut in pending:
-            out = torch.empty_like(buf)
-            for g, i in zip(grads, idx):
-                off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
-                out[off:off + g.numel()].view(g.shape).copy_(outs[i])
-            fut.set_result(out)
+        flat = torch.cat([o.reshape(-1) for o in outs])  # the averages in the state's order
+        for buf, gidx, fut in pending:
+            fut.set_result(flat.index_select(0, gidx))  # one gather per bucket, in its layout
 
 
 def powersgd_hook(state: PowerSGDState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:

@@ -51,10 +51,12 @@ def _state(params, codec):
     st.params = params
     st._index = {id(p): i for i, p in enumerate(params)}
     st.residual = torch.zeros(sum(p.numel() for p in params))
-    st.views, off = [], 0
+    st.views, st._offs, off = [], [], 0
     for p in params:
+        st._offs.append(off)
         st.views.append(st.residual[off:off + p.numel()].view(p.shape))
         off += p.numel()
+    st._gidx = {}
     st.powersgd = codec
     st._seen = [False] * len(params)
     st._nseen = 0
