@@ -35,15 +35,9 @@ template <int R>
 struct FinRB {
     static constexpr int value = R == 4 ? 1 : PSGD_FIN_RB12;
 };
-// Threads per workgroup: 512 at ranks 2 and 4 (a row spread over twice the threads keeps the
-// per-thread panels small enough for two waves per SIMD on rows of up to ~12k columns, e.g. the
-// 11008-column Llama MLP rows at rank 2), else 256
-#ifndef PSGD_FIN_NT2
-#define PSGD_FIN_NT2 512
-#endif
 template <int R>
 struct FinNT {
-    static constexpr int value = R == 4 ? 512 : R == 2 ? PSGD_FIN_NT2 : 256;
+    static constexpr int value = R == 4 ? 512 : 256;
 };
 
 // Gradient / output rows go through buffer descriptors spanning exactly one matrix: a
@@ -563,8 +557,6 @@ hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, 
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
     if constexpr (R <= 2) {
         if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
-        if (smax <= 8 && nres <= 1)
-            return nres == 0 ? launch_final_k<T, R, 8, 0>(a, ntiles, s, waves) : launch_final_k<T, R, 8, 1>(a, ntiles, s, waves);
         if (smax <= 12 && (nres <= 1 || nres == kFinProj)) {
             if (nres == kFinProj) return launch_final_k<T, R, 12, 0, true>(a, ntiles, s, waves);
             return nres == 0 ? launch_final_k<T, R, 12, 0>(a, ntiles, s, waves)
