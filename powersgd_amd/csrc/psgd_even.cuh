@@ -31,11 +31,6 @@ namespace psgd {
 #ifndef PSGD_EVEN_U
 #define PSGD_EVEN_U 4
 #endif
-// cache policy bits of the full-run partial stores (0: plain; gfx950 CPol sc0 = 1, nt = 2,
-// sc1 = 16): A/B knob for write-through partials that the reduction reads on other XCDs
-#ifndef PSGD_PART_AUX
-#define PSGD_PART_AUX 0
-#endif
 constexpr int kEvenNT = PSGD_EVEN_NT;
 constexpr int kEvenNW = kEvenNT / 64;
 constexpr int kEvenU = PSGD_EVEN_U;
@@ -124,14 +119,7 @@ __device__ __forceinline__ void even_epilogue(const ProductArgs& a, const Seg& s
             v4f s = *reinterpret_cast<const v4f*>(red + i4);
 #pragma unroll
             for (int w = 1; w < kEvenNW; ++w) s += *reinterpret_cast<const v4f*>(red + w * width + i4);
-            if constexpr (PSGD_PART_AUX != 0) {  // cache policy of the partial slab (A/B knob)
-                typedef unsigned v4u __attribute__((ext_vector_type(4)));
-                const v4u x = {__float_as_uint(s.x), __float_as_uint(s.y), __float_as_uint(s.z), __float_as_uint(s.w)};
-                __builtin_amdgcn_raw_buffer_store_b128(x, make_rsrc(a.part + sg.part, uint32_t(width) * 4u),
-                                                       uint32_t(i4) * 4u, 0, PSGD_PART_AUX);
-            } else {
-                *(gptr<v4f>)(part + i4) = s;
-            }
+            *(gptr<v4f>)(part + i4) = s;
         }
     } else {
         for (int idx = tid; idx < width; idx += kEvenNT) {
