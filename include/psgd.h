@@ -188,9 +188,9 @@ int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step,
 /* Nonzero when the last iteration of `step` is odd and every matrix fits the fused final
  * pass (row-resident product + residual, psgd_final.cuh). aggregate = 0: the building-block
  * path (psgd_compress of that iteration then writes the residual); aggregate = 1:
- * psgd_aggregate, which also fuses two-iteration rank-2/4 plans in the projection form
+ * psgd_aggregate, which also fuses two-iteration rank-1/2/4 plans in the projection form
  * (output G X X^T, exact for I = 2 at world size 1): *fused = 2 for that
- * form (k_final_proj), 1 for the K-term form (k_final_odd / k_final_lds), 0 unfused. */
+ * form (k_final_proj; ranks 1/2/4), 1 for the K-term form (k_final_odd), 0 unfused. */
 int psgd_plan_fused_final(const psgd_plan* plan, int64_t step, int32_t aggregate, int32_t* fused);
 
 /* Kernel timing for benchmarks: when enabled, every final pass launched by psgd_aggregate
