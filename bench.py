@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true",
                     help="N = 1: skip the rank-4 block and the world-size > 1 path block (1-rank RCCL group)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the cross-GPU parity check of the W > 1 transports (after the timed blocks)")
     ap.add_argument("--launch-check", action="store_true",
                     help="rendezvous + world-size report only (no codec; CPU-testable with gloo)")
     return ap.parse_args()
@@ -234,13 +236,19 @@ def main():
     if world > 1 and backend == "nccl" and "PSGD_COMM_BUCKETS" not in os.environ:
         # the RCCL step with 2 buckets: each bucket's collective under the next bucket's kernels
         out["rccl_buckets2"] = env_block(a, world, rank, dev, backend, {"PSGD_COMM_BUCKETS": "2"})
+    if world > 1 and not a.no_parity:
+        # correctness of the cross-device run itself (after every timed block)
+        out["multi_gpu_parity"] = multi_gpu_parity(world, rank, dev, backend)
     if rank == 0 and world == 1 and not a.no_extra:
         # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
         # world size 1, cold, same steps
+        # the real caller's cache state: autograd's accumulation into p.grad just before
+        out["post_backward"] = post_backward(a, a.config, dev)
         if a.config != "cfg3_resnet50_r4":
             r4 = measure(a, "cfg3_resnet50_r4", 1, 0, dev, backend, "cold")
             out["rank4"] = {k: r4[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
             out["rank4"]["config"] = r4["config"]
+            out["rank4"]["post_backward"] = post_backward(a, "cfg3_resnet50_r4", dev)
         # the world-size > 1 code path (bucketed async factor all-reduces, per-bucket kernels,
         # write-only output pass) timed on this one GPU through a 1-rank RCCL group: the
         # per-rank compute floor of every multi-GPU point (no xGMI traffic: one rank)
@@ -264,6 +272,180 @@ def CONFIGS_():
     from powersgd_amd.workloads import CONFIGS
 
     return CONFIGS
+
+
+# ------------------------------------------------------------------ multi-GPU parity (N > 1)
+# The driver's N > 1 run is the only cross-device execution of the W > 1 transports, so after
+# every timed block (never inside one) each transport runs PARITY_STEPS steps of the ResNet-50
+# configs from one common injected P/Q state; every rank's outputs and residuals are gathered to
+# rank 0 and compared with W reference workers (oracle/multiworker.py: the CPU restatement of the
+# reference, W threads meeting at the reference's SUM all-reduce, powersgd.py:204-219). The
+# oracle is the checker here, never the thing measured.
+PARITY_STEPS = 2
+PARITY_CFGS = ("cfg2_resnet50_r1", "cfg3_resnet50_r4")
+PARITY_TOL = (1e-5, 1e-4)  # step 0 (same state), step 1 (free-running)
+
+
+def parity_inputs(shapes, rank, t):
+    """Rank `rank`'s fresh gradient of step t (CPU fp32, seeded: rank 0 regenerates every rank's)."""
+    g = torch.Generator().manual_seed(7919 * (rank + 1) + 104729 * (t + 1))
+    return [torch.randn(s, generator=g) for s in shapes]
+
+
+def gather_to_rank0(t, world, rank, backend):
+    """Every rank's 1-D tensor, in rank order, on rank 0 (CPU); None on the other ranks."""
+    if backend == "nccl":
+        parts = [torch.empty_like(t) for _ in range(world)]
+        torch.distributed.all_gather(parts, t)
+        return [p.cpu() for p in parts] if rank == 0 else None
+    t = t.detach().cpu()
+    parts = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    torch.distributed.gather(t, parts, dst=0)
+    return parts
+
+
+def parity_collect(step, shapes, world, rank, backend, dev):
+    """PARITY_STEPS steps of `step(grads) -> outs` on this rank (error feedback: the residual
+    left in `grads` + the next fresh gradient), then the gathers. Every rank makes the same
+    collectives even if its steps failed (its rows are NaN then), so a failure cannot hang the
+    others. Returns (outs[t][w], residuals[t][w], errors[w]) on rank 0."""
+    total = sum(numel(s) for s in shapes)
+    flats, err = [], None
+    try:
+        res = [torch.zeros(s, device=dev) for s in shapes]
+        for t in range(PARITY_STEPS):
+            g = [r + x.to(dev) for r, x in zip(res, parity_inputs(shapes, rank, t))]
+            o = step(g)
+            flats.append((torch.cat([x.reshape(-1).float() for x in o]), torch.cat([x.reshape(-1).float() for x in g])))
+            res = g
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+    except Exception as e:  # reported, not raised: the other ranks still gather
+        err = f"{type(e).__name__}: {str(e)[:300]}"
+        flats = [(torch.full((total,), float("nan"), device=dev),) * 2 for _ in range(PARITY_STEPS)]
+    errs = [None] * world
+    torch.distributed.all_gather_object(errs, err)
+    outs = [gather_to_rank0(o, world, rank, backend) for o, _ in flats]
+    ress = [gather_to_rank0(r, world, rank, backend) for _, r in flats]
+    return outs, ress, errs
+
+
+def parity_check(c, world, p0, q0, outs, ress):
+    """Rank 0: the reference's W-worker steps on the same inputs from the same P/Q state; the
+    largest per-tensor error relative to that rank's input tensor (SURVEY §8(c) metric)."""
+    from oracle import multiworker as MW
+    from oracle import powersgd_oracle as O
+
+    shapes = c["shapes"]
+    sizes = [numel(s) for s in shapes]
+    states = []
+    for _ in range(world):
+        st = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
+        st.codec.p_flat.copy_(p0)
+        st.codec.q_flat.copy_(q0)
+        states.append(st)
+    res = [[torch.zeros(s) for s in shapes] for _ in range(world)]
+    steps, ok, same = [], True, True
+    for t in range(PARITY_STEPS):
+        grads = [[r + x for r, x in zip(res[w], parity_inputs(shapes, w, t))] for w in range(world)]
+        scale = [[max(float(g.norm()), 1e-30) for g in gw] for gw in grads]
+        want = MW.run_workers(states, grads)
+        eo = er = 0.0
+        for w in range(world):
+            got_o = torch.split(outs[t][w], sizes)
+            got_r = torch.split(ress[t][w], sizes)
+            for i in range(len(shapes)):
+                eo = max(eo, float((got_o[i] - want[w][i].reshape(-1)).norm()) / scale[w][i])
+                er = max(er, float((got_r[i] - grads[w][i].reshape(-1)).norm()) / scale[w][i])
+            same = same and torch.equal(outs[t][w], outs[t][0])
+        tol = PARITY_TOL[min(t, 1)]
+        ok = ok and eo <= tol and er <= tol  # NaN compares False
+        steps.append({"max_rel_out": float(f"{eo:.3e}"), "max_rel_res": float(f"{er:.3e}"), "tol": tol})
+        res = grads
+    return {"ok": ok, "outputs_equal_on_all_ranks": same, "steps": steps}
+
+
+def multi_gpu_parity(world, rank, dev, backend):
+    """Each W > 1 transport (RCCL in the library and the IPC exchange on the nccl backend;
+    torch.distributed and the IPC exchange on gloo) on the ResNet-50 configs, checked on rank 0."""
+    from powersgd_amd import Config, PowerSGD
+
+    transports = ("rccl", "ipc") if backend == "nccl" else ("torch", "ipc")
+    report = {"steps": PARITY_STEPS, "world": world,
+              "note": "every rank's outputs/residuals vs W reference workers from one injected P/Q state"}
+    for tr in transports:
+        old = os.environ.get("PSGD_COMM")
+        os.environ["PSGD_COMM"] = tr
+        report[tr] = {}
+        try:
+            for cfg in PARITY_CFGS:
+                c = CONFIGS_()[cfg]
+                psgd = PowerSGD([torch.zeros(s, device=dev) for s in c["shapes"]],
+                                Config(c["rank"], c["mcr"], c["iters"], 0))
+                codec = psgd._powersgd
+                for buf in (codec._ps_buffer, codec._qs_buffer):  # one common injected state
+                    host = buf.cpu()
+                    torch.distributed.broadcast(host if backend != "nccl" else buf, src=0)
+                    if backend != "nccl":
+                        buf.copy_(host)
+                p0, q0 = codec._ps_buffer.cpu(), codec._qs_buffer.cpu()
+                outs, ress, errs = parity_collect(psgd.aggregate, c["shapes"], world, rank, backend, dev)
+                try:
+                    codec.close()
+                except RuntimeError as e:
+                    errs = errs + [str(e)[:200]]
+                if rank == 0:
+                    r = parity_check(c, world, p0, q0, outs, ress)
+                    if any(errs):
+                        r["ok"] = False
+                        r["errors"] = [e for e in errs if e]
+                    report[tr][cfg] = r
+                del psgd, codec
+                torch.cuda.empty_cache()
+        finally:
+            if old is None:
+                os.environ.pop("PSGD_COMM", None)
+            else:
+                os.environ["PSGD_COMM"] = old
+    if rank == 0:
+        report["ok"] = all(report[tr][cfg]["ok"] for tr in transports for cfg in PARITY_CFGS)
+    return report
+
+
+def post_backward(a, cfg_name, dev):
+    """The real caller's cache state (reference README.md:39-42: ``loss.backward()`` accumulates
+    the fresh gradient into ``p.grad``, which holds the residual, right before ``aggregate``).
+    Per step an in-stream foreach add of a fresh gradient set into the gradients, then one
+    aggregate; CUDA events on torch's current stream (the codec's launch stream) bracket the
+    aggregate alone, so the add is not counted but its cache footprint is."""
+    from powersgd_amd import Config, PowerSGD
+
+    c = dict(CONFIGS_()[cfg_name])
+    dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+    shapes = c["shapes"]
+    gen = torch.Generator(device=dev).manual_seed(4321)
+    grads = [torch.randn(s, generator=gen, device=dev, dtype=torch.float32).to(dtype) for s in shapes]
+    fresh = [torch.randn(s, generator=gen, device=dev, dtype=torch.float32).to(dtype) for s in shapes]
+    psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dtype) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+    for _ in range(a.warmup):
+        torch._foreach_add_(grads, fresh)
+        psgd.aggregate(grads)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    for k in range(a.steps):
+        torch._foreach_add_(grads, fresh)  # autograd's accumulation into p.grad (the residual)
+        evs[k][0].record()
+        psgd.aggregate(grads)
+        evs[k][1].record()
+    torch.cuda.synchronize()
+    ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    s = 2 if dtype == torch.bfloat16 else 4
+    byts = sum(numel(x) for x in shapes) * s
+    del grads, fresh, psgd
+    torch.cuda.empty_cache()
+    return {"ms_per_step": round(ms, 4), "value": round(byts / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+            "note": "in-stream grad += fresh (autograd accumulation) before each aggregate; events around "
+                    "aggregate only"}
 
 
 def ipc_block(a, world, rank, dev, backend):

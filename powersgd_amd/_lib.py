@@ -234,7 +234,8 @@ class Plan:
                                        stream))
 
     def ipc_status(self) -> bool:
-        """True if a device-side wait timed out since the last call (synchronous)."""
+        """True if a device-side wait timed out since the exchange was opened (synchronous; sticky
+        until ipc_close: every later aggregate_ipc raises)."""
         v = _i32()
         check(lib().psgd_ipc_status(self._h, ctypes.byref(v)))
         return bool(v.value)

@@ -20,6 +20,11 @@ struct psgd_comm {
     // ordered against the codec's stream with events (kernels of bucket b+1 overlap bucket b's
     // collective)
     hipStream_t cs = nullptr;
+    // set by the first failed collective: the ranks' call sequences have diverged, so every
+    // later call fails at once (PSGD_ERR_STATE) instead of enqueueing into a communicator whose
+    // peers are waiting on a different collective (a hang elsewhere)
+    bool poisoned = false;
+    std::string poison;
 };
 
 namespace psgd {
@@ -48,7 +53,8 @@ Rccl load() {
     if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
     if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
     if (!h) {
-        r.error = std::string("cannot load librccl.so: ") + (dlerror() ? dlerror() : "?");
+        const char* de = dlerror();  // read once: a second call returns null
+        r.error = std::string("cannot load librccl.so: ") + (de ? de : "?");
         return r;
     }
     auto sym = [&](const char* n) { return dlsym(h, n); };
@@ -79,6 +85,12 @@ int rccl_fail(ncclResult_t e, const char* what) {
 
 int comm_world(const psgd_comm* c) { return c->world; }
 
+void comm_poison(psgd_comm* c, const char* why) {
+    if (c->poisoned) return;
+    c->poisoned = true;
+    c->poison = why ? why : "?";
+}
+
 hipStream_t comm_stream(psgd_comm* c) {
     if (!c->cs) {
         int prev = -1;
@@ -93,13 +105,24 @@ hipStream_t comm_stream(psgd_comm* c) {
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s) {
     const Rccl& r = rccl();
     if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
+    if (c->poisoned) return comm_fail(PSGD_ERR_STATE, ("communicator unusable after an earlier failure: " + c->poison).c_str());
     ncclResult_t e = r.group_start();
-    if (e != ncclSuccess) return rccl_fail(e, "ncclGroupStart");
-    if (n) e = r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, s);
-    if (e == ncclSuccess && n2) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
-    const ncclResult_t e2 = r.group_end();
-    if (e != ncclSuccess) return rccl_fail(e, "ncclAllReduce");
-    if (e2 != ncclSuccess) return rccl_fail(e2, "ncclGroupEnd");
+    const char* what = "ncclGroupStart";
+    if (e == ncclSuccess) {
+        what = "ncclAllReduce";
+        if (n) e = r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, s);
+        if (e == ncclSuccess && n2) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
+        const ncclResult_t e2 = r.group_end();
+        if (e == ncclSuccess && e2 != ncclSuccess) {
+            e = e2;
+            what = "ncclGroupEnd";
+        }
+    }
+    if (e != ncclSuccess) {
+        c->poisoned = true;
+        c->poison = std::string(what) + ": " + (r.error_string ? r.error_string(e) : "?");
+        return rccl_fail(e, what);
+    }
     return PSGD_OK;
 }
 

@@ -335,7 +335,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             a.yloc[e] = y;
                             a.state[e] = y;
                             if constexpr (!PJ) {  // the exchange (W > 1) never takes the projection form
-                                if (a.xout) a.xout[e] = y;
+                                if (a.xout) st_slot(a.xout + e, y);
                             }
                         }
                 }

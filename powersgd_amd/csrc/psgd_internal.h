@@ -15,6 +15,7 @@ int comm_fail(int code, const char* msg);
 int comm_world(const psgd_comm* c);
 hipStream_t comm_stream(psgd_comm* c);  // created on first use; null if creation failed
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
+void comm_poison(psgd_comm* c, const char* why);  // every later comm_allreduce fails (PSGD_ERR_STATE)
 
 // Benchmark timing of the final pass (psgd_plan_set_timing): while set, the final-pass launch
 // records these events from its own dispatch packet (hipExtLaunchKernel), so the measured span

@@ -451,7 +451,13 @@ struct psgd_plan {
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
     int64_t ipc_slot = 0, ipc_flat_off = 0, ipc_flat_cap = 0;
-    size_t o_ipc_ptrs = 0, o_xerr = 0;
+    size_t o_ipc_ptrs = 0;
+    // sticky timeout word of the exchange waits: pinned host memory mapped into the device
+    // (k_xchg stores 1 with a system-scope store), so every psgd_aggregate_ipc call can check it
+    // without synchronising; cleared only by psgd_ipc_close
+    int32_t* xerr_host = nullptr;
+    int32_t* xerr_dev = nullptr;
+    bool xerr_set() const { return xerr_host && __atomic_load_n(xerr_host, __ATOMIC_ACQUIRE) != 0; }
     float* xout_now = nullptr;  // set per iteration by psgd_aggregate_ipc (exchange slot)
     // history slot of the RAW in-factor the rank-1 norm fold reads: 1 (the local reduction's
     // output, world size 1) or 2 (the exchange's summed copy, psgd_aggregate_ipc)
@@ -483,6 +489,7 @@ struct psgd_plan {
         for (size_t w = 0; w < ipc_peer.size(); ++w)
             if (ipc_peer[w] && int(w) != ipc_rank) (void)hipIpcCloseMemHandle(ipc_peer[w]);
         if (ipc_buf) (void)hipFree(ipc_buf);  // peers must have closed it first (psgd_ipc_close)
+        if (xerr_host) (void)hipHostFree(xerr_host);
     }
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
@@ -1153,7 +1160,6 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
     p->o_ipc_ptrs = carve(size_t(kMaxRanks) * sizeof(void*));
-    p->o_xerr = carve(sizeof(int32_t));
     p->o_rq = carve(size_t(std::max<int64_t>(p->fmax, 1)) * sizeof(float));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
@@ -1694,7 +1700,12 @@ int psgd_ipc_create(psgd_plan* p, int64_t flat_numel, void* handle_out) {
     const size_t bytes = size_t(kXchgHeader) + size_t(2 * p->iters * p->ipc_slot) * sizeof(float);
     PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->ipc_buf), bytes));
     PSGD_HIP(hipMemset(p->ipc_buf, 0, bytes));  // flags at epoch 0
-    PSGD_HIP(hipMemset(p->dev<int32_t>(p->o_xerr), 0, sizeof(int32_t)));
+    if (!p->xerr_host) {
+        PSGD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->xerr_host), sizeof(int32_t),
+                               hipHostMallocMapped | hipHostMallocCoherent));
+        PSGD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->xerr_dev), p->xerr_host, 0));
+    }
+    __atomic_store_n(p->xerr_host, 0, __ATOMIC_RELEASE);
     PSGD_HIP(hipDeviceSynchronize());  // zeroed before any peer can open and poll it
     PSGD_HIP(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), p->ipc_buf));
     return PSGD_OK;
@@ -1736,6 +1747,7 @@ int psgd_ipc_close(psgd_plan* p) {
     p->ipc_peer.clear();
     p->ipc_world = 0;
     p->ipc_rank = -1;
+    if (p->xerr_host) __atomic_store_n(p->xerr_host, 0, __ATOMIC_RELEASE);  // a fresh exchange
     return PSGD_OK;
 }
 
@@ -1743,11 +1755,8 @@ int psgd_ipc_status(psgd_plan* p, int32_t* timed_out) {
     if (!p || !timed_out) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     DevScope scope(p->device);
-    int32_t v = 0;
-    PSGD_HIP(hipDeviceSynchronize());
-    PSGD_HIP(hipMemcpy(&v, p->dev<int32_t>(p->o_xerr), sizeof(v), hipMemcpyDeviceToHost));
-    if (v) PSGD_HIP(hipMemset(p->dev<int32_t>(p->o_xerr), 0, sizeof(int32_t)));
-    *timed_out = v;
+    PSGD_HIP(hipDeviceSynchronize());  // every enqueued exchange wait has ended
+    *timed_out = p->xerr_set() ? 1 : 0;  // sticky until psgd_ipc_close
     return PSGD_OK;
 }
 
@@ -2035,6 +2044,9 @@ int psgd_aggregate_flat(psgd_plan* p, void* const* grads, void* out, int64_t ste
     return aggregate_entry(p, grads, out, step, s, &a, f);
 }
 
+static int aggregate_comm_body(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f,
+                               void* const* unc, void* flat_out, psgd_comm* comm, hipStream_t s);
+
 // World size W in one call (include/psgd.h): per iteration the kernels, then the in-place SUM
 // all-reduce of the out-factor state on the same stream (the last grouped with the flat
 // buffer of the uncompressed tensors), then the output pass. Same sequence as the building
@@ -2053,7 +2065,18 @@ int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t ste
         if (f->dtype != PSGD_F32) return fail(PSGD_ERR_DTYPE, "psgd_aggregate_comm packs fp32 uncompressed tensors");
     }
     DevScope scope(p->device);
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int st = aggregate_comm_body(p, grads, out, step, has_flat ? f : nullptr, unc, flat_out, comm,
+                                       static_cast<hipStream_t>(stream));
+    // a failure past the argument checks can leave this rank's collective sequence short of its
+    // peers': the communicator refuses every later call (psgd_comm.cpp, comm_poison)
+    if (st) comm_poison(comm, psgd_last_error());
+    return st;
+}
+
+static int aggregate_comm_body(psgd_plan* p, void* const* grads, void* out, int64_t step, psgd_flat* f,
+                               void* const* unc, void* flat_out, psgd_comm* comm, hipStream_t s) {
+    void* stream = s;
+    const bool has_flat = f != nullptr;
     const int world = comm_world(comm);
     // x / W into the flat buffer, x = 0 (utils.py:43-47, powersgd.py:29-30): inside the first
     // even product's launch when the step starts even, else its own launch
@@ -2122,6 +2145,11 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
     if (!p || !grads || !out) return fail(PSGD_ERR_VALUE, "null argument");
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "psgd_ipc_open first");
+    // a wait of an earlier step gave up: that step's sums were invalid and the two-parity slot
+    // reuse is no longer safe, so every later step is refused (the ranks have drifted apart)
+    if (p->xerr_set())
+        return fail(PSGD_ERR_STATE, "an earlier IPC exchange wait timed out (a peer did not arrive within "
+                                    "PSGD_IPC_SPIN); the exchange is invalid until psgd_ipc_close");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     const bool has_flat = f && f->total > 0;
@@ -2195,7 +2223,7 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
         xa.spin_limit = spin;
         xa.world = world;
         xa.rank = p->ipc_rank;
-        xa.err = p->dev<int32_t>(p->o_xerr);
+        xa.err = p->xerr_dev;
         PSGD_HIP(launch_xchg(xa, s));
     }
     return decompress_impl(p, grads, out, step, world, s, false);

@@ -1842,7 +1842,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         if (e < cnt) {
             a.yloc[dbase + e] = t;
             a.state[dbase + e] = t;
-            if (a.xout) a.xout[dbase + e] = t;
+            if (a.xout) st_slot(a.xout + dbase + e, t);
             sq = fmaf(t, t, sq);
             tv[j] = t;
         }
@@ -1899,13 +1899,21 @@ hipError_t launch_reduce(const ReduceArgs& a, int nitems, hipStream_t s) {
 
 // ---------------------------------------------------------------- one-shot all-reduce
 // The reference's SUM all-reduce of an out-factor (powersgd.py:204-209), one node, one
-// process per GPU, stream-ordered with no host round trip: the kernels before this one left the
-// LOCAL factor in this rank's exchange slot (their completion on this stream makes it visible
-// device-wide); workgroup 0 raises this rank's epoch flag for the iteration (system-scope
-// release), then every workgroup polls the peers' flags (system-scope loads, bounded: a peer
-// that never arrives sets a.err instead of hanging the queue) and sums its share of the W slots
-// in rank order, so every rank computes bitwise the same values. Peer data is read with
-// system-scope loads: no stale line a previous step left in this XCD's caches can be hit.
+// process per GPU, stream-ordered with no host round trip. Cross-GPU visibility, step by step:
+//  1. the kernels before this one wrote the LOCAL factor into this rank's exchange slot with
+//     system-scope stores (st_slot: `sc0 sc1`, write-through; the flat region with PSGD_ST_AUX
+//     = sc0 | nt | sc1): no byte of the slot waits in any of the eight L2s for a writeback;
+//  2. this launch starts only after they completed (same stream, barrier bit): every one of those
+//     stores has been acknowledged by memory;
+//  3. workgroup 0 then stores this rank's epoch flag (system scope, `sc0 sc1`);
+//  4. peers poll the flag with system-scope loads and read the slot ONLY with system-scope loads
+//     (`sc0 sc1`, which no non-coherent cache level serves), so they see the bytes of (1).
+// This is the write-through hand-off of MI355X_MICROARCH.md (visibility table, first row: stores
+// all write-through, drained before ONE lane's flag store, flag polled and payload loaded with
+// coherent loads) at system scope, with the kernel boundary as the drain. It needs no release
+// fence: one here would write back only this workgroup's XCD L2, which (1) leaves clean.
+// The wait is bounded: a peer that never arrives sets the sticky error word (host-mapped, read by
+// the next psgd_aggregate_ipc call, which then fails) instead of hanging the queue.
 #ifndef PSGD_XCHG_FLAG_ORDER
 #define PSGD_XCHG_FLAG_ORDER __ATOMIC_RELAXED
 #endif
@@ -1936,10 +1944,8 @@ __device__ __forceinline__ void xchg_sum_quad(const XchgArgs& a, int64_t src_byt
 
 __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
     const int tid = threadIdx.x;
-    // the slot data were written by the PREVIOUS kernels of this stream: their completion
-    // (kernel-end release, at least agent scope: the L2s written back) already made them visible
-    // to every reader of this GPU's memory, so the flag needs no fence of its own (a release here
-    // would write this XCD's L2 back again), only a store that goes to memory (system scope)
+    // the slot bytes were written through by the PREVIOUS kernels of this stream (steps 1-2
+    // above): the flag is a plain system-scope store, no fence
     if (blockIdx.x == 0 && tid == 0)
         __hip_atomic_store(a.own_flag, a.epoch, PSGD_XCHG_FLAG_ORDER, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid < a.world && tid != a.rank) {  // lane w polls peer w: the W round trips overlap
@@ -1947,7 +1953,9 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
         uint32_t spins = 0;
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
             if (++spins > a.spin_limit) {
-                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // host-mapped sticky word (vector store, system scope): the results of this
+                // step are invalid and the host refuses every later exchange step
+                __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
             __builtin_amdgcn_s_sleep(10);

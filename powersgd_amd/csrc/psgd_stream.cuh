@@ -61,6 +61,16 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 // exec-mask branch and a vmcnt(0) wait per load).
 __device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
 
+// A store into this rank's IPC exchange slot (psgd_aggregate_ipc), which peers read over xGMI
+// with system-scope loads after this kernel has completed and k_xchg has raised the epoch flag.
+// System scope lowers to a vector `global_store_dword ... sc0 sc1`: write-through, the line
+// leaves (is dropped from) this XCD's L2 (MI355X_MICROARCH.md, the store-flavour row of the
+// visibility table), so the peer's read never depends on a writeback of the eight L2s at kernel
+// end. The flat region is written through with PSGD_ST_AUX (sc0 | nt | sc1) for the same reason.
+__device__ __forceinline__ void st_slot(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Streaming outputs (residual, output, flat pack) go through buffer descriptors with an explicit
 // cache policy (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16). Default sc0 | nt | sc1: the
 // 200+ MB a final pass writes must not sit dirty in the Infinity Cache, where the NEXT step's

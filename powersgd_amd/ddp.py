@@ -57,7 +57,9 @@ class PowerSGDState:
             self._offs.append(off)
             self.views.append(self.residual[off:off + p.numel()].view(p.shape))
             off += p.numel()
-        self._gidx: Dict[tuple, torch.Tensor] = {}
+        # per DDP bucket index: (layout key, int32 device index map) of its LATEST layout only
+        # (DDP rebuilds its buckets after the first iteration; the old maps are dropped)
+        self._gidx: Dict[int, tuple] = {}
         self.powersgd = PowerSGD(self.views, config)
         self._seen = [False] * len(self.params)
         self._nseen = 0
@@ -76,7 +78,7 @@ class PowerSGDState:
                     raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
                 idx.append(i)
             buf = bucket.buffer()
-            gidx = self._gather_index(buf, grads, idx)
+            gidx = self._gather_index(bucket.index(), buf, grads, idx)
             # error feedback: residual + fresh gradient, the whole bucket in one indexed add
             # (bucket buffer position -> residual position; every position once)
             self.residual.index_add_(0, gidx, buf)
@@ -110,17 +112,23 @@ class PowerSGDState:
         if not fut.done():
             fut.set_exception(err)
 
-    def _gather_index(self, buf: torch.Tensor, grads, idx) -> torch.Tensor:
+    def _gather_index(self, bucket_index: int, buf: torch.Tensor, grads, idx) -> torch.Tensor:
         """Device index: position k of the bucket's flat buffer -> its position in the state's
-        flat residual (built once per bucket layout; DDP rebuilds its buckets once)."""
+        flat residual. int32 (4 bytes per gradient element: index_add_ / index_select take it),
+        built once per bucket layout; only the bucket's latest layout is kept."""
         key = (buf.numel(), tuple(idx), tuple((g.data_ptr() - buf.data_ptr()) // buf.element_size() for g in grads))
-        gidx = self._gidx.get(key)
-        if gidx is None:
-            host = torch.empty(buf.numel(), dtype=torch.long)
-            for g, i in zip(grads, idx):
-                off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
-                host[off:off + g.numel()] = torch.arange(self._offs[i], self._offs[i] + g.numel())
-            gidx = self._gidx[key] = host.to(buf.device)
+        hit = self._gidx.get(bucket_index)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        if self.residual.numel() >= 2 ** 31:
+            raise RuntimeError("powersgd_hook: more than 2^31 gradient elements (int32 index maps)")
+        host = torch.empty(buf.numel(), dtype=torch.int32)
+        for g, i in zip(grads, idx):
+            off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
+            host[off:off + g.numel()] = torch.arange(self._offs[i], self._offs[i] + g.numel(), dtype=torch.int32)
+        self._gidx.pop(bucket_index, None)  # free the stale layout's map before the new upload
+        gidx = host.to(buf.device)
+        self._gidx[bucket_index] = (key, gidx)
         return gidx
 
     def _complete(self) -> None:
@@ -128,9 +136,12 @@ class PowerSGDState:
         pending, self._pending = self._pending, []
         self._seen = [False] * len(self.params)
         self._nseen = 0
-        flat = torch.cat([o.reshape(-1) for o in outs])  # the averages in the state's order
+        # the averages in the state's order (a transient copy: the compressed and uncompressed
+        # outputs live in two buffers), then one gather per bucket, in its layout
+        flat = torch.cat([o.reshape(-1) for o in outs])
         for buf, gidx, fut in pending:
-            fut.set_result(flat.index_select(0, gidx))  # one gather per bucket, in its layout
+            fut.set_result(flat.index_select(0, gidx))
+        del flat
 
 
 def powersgd_hook(state: PowerSGDState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:

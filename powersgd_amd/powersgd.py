@@ -213,6 +213,10 @@ class PowerSGD(Aggregator):
                 outs = outs + self._unc.run(self._table.unc_addr())
         return [outs[i] for i in self._order]  # reference _merge :86-99
 
+    def close(self) -> None:
+        """Collective: release the codec's multi-GPU transports (BasicPowerSGD.close)."""
+        self._powersgd.close()
+
     def _aggregate_merged(self) -> List[torch.Tensor]:
         """World size > 1: ONE collective fewer per step. The uncompressed gradients
         (divided by W, reference utils.py:43-47) are packed behind the factor the last
@@ -346,18 +350,33 @@ class BasicPowerSGD(Aggregator):
                 self._plan.ipc_close()
             raise RuntimeError(f"IPC exchange setup failed on rank(s) {bad}")
         self._ipc_open = True
+        _register_exit_close(self)
 
     def ipc_status(self) -> bool:
         """True if a device-side exchange wait timed out since the last call (synchronous)."""
         return self._ipc_open and self._plan.ipc_status()
 
-    def close_ipc(self) -> None:
+    def close_ipc(self, timeout: Optional[float] = None) -> None:
         """Collective teardown of the IPC exchange: unmap the peers' buffers, then a barrier, so
-        that no rank frees its exchange buffer while a peer still maps it (include/psgd.h)."""
+        that no rank frees its exchange buffer while a peer still maps it (include/psgd.h).
+        ``timeout`` (seconds) bounds the barrier (the exit hook uses it: a rank that died must not
+        hang the others at exit)."""
         if self._ipc_open:
             self._plan.ipc_close()
             self._ipc_open = False
-            torch.distributed.barrier()
+            if timeout is None:
+                torch.distributed.barrier()
+            else:
+                import datetime
+
+                torch.distributed.barrier(async_op=True).wait(datetime.timedelta(seconds=timeout))
+
+    def close(self) -> None:
+        """Release the multi-GPU transports (collective: every rank calls it). The exchange
+        buffers of PSGD_COMM=ipc are unmapped and the ranks meet at a barrier before any frees
+        its buffer; without this call an exit hook does the same with a bounded barrier."""
+        self.close_ipc()
+        self._comm = None
 
     def _rccl_comm(self) -> Optional["_lib.Comm"]:
         """World size > 1 on the NCCL (RCCL) backend: a communicator the library drives itself on
@@ -517,6 +536,32 @@ class BasicPowerSGD(Aggregator):
     @property
     def compression_rate(self) -> float:
         return self.uncompressed_num_floats / self.compressed_num_floats
+
+
+_EXIT_CLOSE: "weakref.WeakSet" = None
+
+
+def _register_exit_close(codec: "BasicPowerSGD") -> None:
+    """At interpreter exit, close every still-open IPC exchange collectively (bounded barrier),
+    so that a rank that finishes first does not free an exchange buffer a slower peer's last
+    exchange kernel may still read (the peers unmap before anyone frees)."""
+    global _EXIT_CLOSE
+    if _EXIT_CLOSE is None:
+        import atexit
+        import weakref
+
+        _EXIT_CLOSE = weakref.WeakSet()
+
+        def _close_all():
+            for c in list(_EXIT_CLOSE):
+                try:
+                    if c._ipc_open and torch.distributed.is_initialized():
+                        c.close_ipc(timeout=float(os.environ.get("PSGD_IPC_EXIT_TIMEOUT", "30")))
+                except Exception:  # exit path: never raise
+                    pass
+
+        atexit.register(_close_all)
+    _EXIT_CLOSE.add(codec)
 
 
 def _views(buf: torch.Tensor, shapes) -> List[torch.Tensor]:

@@ -11,7 +11,8 @@ from powersgd_amd.ddp import PowerSGDState, powersgd_hook
 class _Bucket:
     """The GradBucket surface the hook uses."""
 
-    def __init__(self, params, last):
+    def __init__(self, params, last, index=None):
+        self._index = int(last) if index is None else index
         self._params = params
         self._grads = [torch.ones_like(p) for p in params]
         self._buf = torch.cat([g.view(-1) for g in self._grads])
@@ -34,6 +35,9 @@ class _Bucket:
 
     def is_last(self):
         return self._last
+
+    def index(self):
+        return self._index
 
 
 class _Codec:
@@ -117,3 +121,20 @@ def test_unknown_parameter_and_double_arrival():
     with pytest.raises(RuntimeError):
         f1.wait()
     assert st._nseen == 0
+
+
+def test_index_maps_are_int32_and_only_the_latest_layout_is_kept():
+    """A DDP bucket rebuild (new layout under the same bucket index) replaces that bucket's
+    index map; maps are int32 (4 bytes per gradient element)."""
+    ps = _params()
+    st = _state(ps, _Codec())
+    powersgd_hook(st, _Bucket(ps[:2], False, index=0))
+    powersgd_hook(st, _Bucket(ps[2:], True, index=1))
+    assert sorted(st._gidx) == [0, 1] and all(v[1].dtype == torch.int32 for v in st._gidx.values())
+    # rebuilt buckets: parameter 2 moves into bucket 0
+    f0 = powersgd_hook(st, _Bucket([ps[2], ps[0]], False, index=0))
+    f1 = powersgd_hook(st, _Bucket(ps[1:2], True, index=1))
+    assert sorted(st._gidx) == [0, 1]
+    assert st._gidx[0][1].numel() == 16 and st._gidx[1][1].numel() == 8
+    # the stub codec leaves the residual in place: two iterations of ones accumulated
+    assert torch.equal(f0.value(), torch.full((16,), 2.)) and torch.equal(f1.value(), torch.full((8,), 2.))

@@ -88,8 +88,12 @@ def _timeout_worker(rank_id, initfile):
             psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
             torch.cuda.synchronize()
             assert psgd._powersgd.ipc_status()
-            assert not psgd._powersgd.ipc_status()  # read-and-clear
+            assert psgd._powersgd.ipc_status()  # sticky: the exchange stays invalid
+            # the next step refuses to run on an invalid exchange instead of returning stale sums
+            with pytest.raises(RuntimeError, match="timed out"):
+                psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
         psgd._powersgd.close_ipc()
+        assert not psgd._powersgd.ipc_status()
     finally:
         torch.distributed.destroy_process_group()
 
@@ -112,22 +116,27 @@ def _one_rank_worker(_, initfile, cfg, steps):
         dev = torch.device("cuda:0")
         c = CONFIGS[cfg]
         shapes = c["shapes"]
-        psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+        dt = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+        psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dt) for s in shapes],
+                        Config(c["rank"], c["mcr"], c["iters"], 0))
         ora = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
         ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
         ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
-        res_d = [torch.zeros(s, device=dev) for s in shapes]
+        res_d = [torch.zeros(s, device=dev, dtype=dt) for s in shapes]
         res_c = [torch.zeros(s) for s in shapes]
         for t in range(steps):
             new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=700 + t)]
-            gd = [r + x.to(dev) for r, x in zip(res_d, new)]
-            gc = [r + x for r, x in zip(res_c, new)]
+            gd = [(r.float() + x.to(dev)).to(dt) for r, x in zip(res_d, new)]
+            # the oracle sees exactly the device inputs (bf16: the rounded values, upcast)
+            gc = [g.float().cpu() for g in gd] if dt == torch.bfloat16 else [r + x for r, x in zip(res_c, new)]
             scale = [g.clone() for g in gc]
             od = psgd.aggregate(gd)
             oc = O.policy_step(ora, gc)
             torch.cuda.synchronize()
             for i, g in enumerate(scale):
                 tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
+                if dt == torch.bfloat16:
+                    tol = 1e-2  # bf16 gradient storage
                 eo = float((od[i].cpu().double() - oc[i].double()).norm()) / max(float(g.norm()), 1e-30)
                 er = float((gd[i].cpu().double() - gc[i].double()).norm()) / max(float(g.norm()), 1e-30)
                 check(eo, tol, cfg, 0, t, i, "ipc1-out")
@@ -139,7 +148,7 @@ def _one_rank_worker(_, initfile, cfg, steps):
         torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", ["cfg2_resnet50_r1", "cfg5_lstm_r1_i4", "cfg3_resnet50_r4"])
+@pytest.mark.parametrize("cfg", ["cfg2_resnet50_r1", "cfg5_lstm_r1_i4", "cfg3_resnet50_r4", "cfg4_llama_r2_bf16"])
 def test_ipc_one_rank_vs_oracle(cfg):
     with tempfile.TemporaryDirectory() as td:
         torch.multiprocessing.spawn(_one_rank_worker, args=(os.path.join(td, "init"), cfg, 3), nprocs=1, join=True)

@@ -32,16 +32,19 @@ def _worker(_, port, cfg, steps, buckets=1):
     try:
         c = CONFIGS[cfg]
         shapes = c["shapes"]
-        psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+        dt = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+        psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dt) for s in shapes],
+                        Config(c["rank"], c["mcr"], c["iters"], 0))
         ora = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
         ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
         ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
-        res_d = [torch.zeros(s, device=dev) for s in shapes]
+        res_d = [torch.zeros(s, device=dev, dtype=dt) for s in shapes]
         res_c = [torch.zeros(s) for s in shapes]
         for t in range(steps):
             new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=900 + t)]
-            gd = [r + x.to(dev) for r, x in zip(res_d, new)]
-            gc = [r + x for r, x in zip(res_c, new)]
+            gd = [(r.float() + x.to(dev)).to(dt) for r, x in zip(res_d, new)]
+            # the oracle sees exactly the device inputs (bf16: the rounded values, upcast)
+            gc = [g.float().cpu() for g in gd] if dt == torch.bfloat16 else [r + x for r, x in zip(res_c, new)]
             scale = [g.clone() for g in gc]
             od = psgd.aggregate(gd)
             oc = O.policy_step(ora, gc)
@@ -51,6 +54,8 @@ def _worker(_, port, cfg, steps, buckets=1):
                 assert psgd._powersgd._buckets is not None and len(psgd._powersgd._buckets) > 1
             for i, g in enumerate(scale):
                 tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
+                if dt == torch.bfloat16:
+                    tol = 1e-2  # bf16 gradient storage
                 check(_rel(od[i], oc[i], g), tol, cfg, t, i, "out")
                 check(_rel(gd[i], gc[i], g), tol, cfg, t, i, "res")
             res_d, res_c = gd, gc
@@ -58,7 +63,7 @@ def _worker(_, port, cfg, steps, buckets=1):
         torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("cfg", ["cfg3_resnet50_r4", "cfg2_resnet50_r1", "cfg5_lstm_r1_i4"])
+@pytest.mark.parametrize("cfg", ["cfg3_resnet50_r4", "cfg2_resnet50_r1", "cfg5_lstm_r1_i4", "cfg4_llama_r2_bf16"])
 def test_rccl_step_one_rank_vs_oracle(cfg):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
