@@ -31,6 +31,11 @@ namespace psgd {
 #ifndef PSGD_EVEN_U
 #define PSGD_EVEN_U 4
 #endif
+// bf16 full-width strips: a lane's 4 columns are one 8-byte load, so a row batch carries half the
+// bytes of fp32's (rows in flight per lane of even_seg_full)
+#ifndef PSGD_EVEN_U_BF16
+#define PSGD_EVEN_U_BF16 PSGD_EVEN_U
+#endif
 constexpr int kEvenNT = PSGD_EVEN_NT;
 constexpr int kEvenNW = kEvenNT / 64;
 constexpr int kEvenU = PSGD_EVEN_U;
@@ -165,7 +170,7 @@ template <typename T, int R, int K>
 __device__ __forceinline__ void even_seg_full(const ProductArgs& a, const Seg& sg, const void* gp, float* red,
                                               float* ssl) {
     constexpr uint32_t s = sizeof(T);
-    constexpr int U = kEvenU;
+    constexpr int U = s == 2 ? PSGD_EVEN_U_BF16 : kEvenU;
     const int lane = threadIdx.x & 63, wave = uni(int32_t(threadIdx.x >> 6));
     const int32_t m = int32_t(sg.m);
     const int32_t col0 = sg.strip * 256 + 4 * lane;
@@ -369,13 +374,27 @@ __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, co
 #ifndef PSGD_EVEN_WPE_R4
 #define PSGD_EVEN_WPE_R4 5
 #endif
-template <int R, int K>
+// bf16 gradients: the narrow-strip paths' 16-bit loads and conversions need more registers; at
+// the fp32 targets the rank-2/4 instances spilled VGPRs to scratch (tools/regs.py), so one wave
+// per SIMD fewer there
+#ifndef PSGD_EVEN_WPE_BF16_R2
+#define PSGD_EVEN_WPE_BF16_R2 5
+#endif
+#ifndef PSGD_EVEN_WPE_BF16_R4
+#define PSGD_EVEN_WPE_BF16_R4 4
+#endif
+template <typename T, int R, int K>
 struct EvenWpe {
-    static constexpr int value = K != 0 ? 1 : R == 1 ? PSGD_EVEN_WPE_R1 : R == 2 ? PSGD_EVEN_WPE_R2 : R == 4 ? PSGD_EVEN_WPE_R4 : 1;
+    static constexpr bool kBf = sizeof(T) == 2;
+    static constexpr int value = K != 0 ? 1
+                                 : R == 1 ? PSGD_EVEN_WPE_R1
+                                 : R == 2 ? (kBf ? PSGD_EVEN_WPE_BF16_R2 : PSGD_EVEN_WPE_R2)
+                                 : R == 4 ? (kBf ? PSGD_EVEN_WPE_BF16_R4 : PSGD_EVEN_WPE_R4)
+                                          : 1;
 };
 
 template <typename T, int R, int K>
-__global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe<R, K>::value))) void k_even(ProductArgs a) {
+__global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value))) void k_even(ProductArgs a) {
     // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees vec == 0)
     __shared__ __attribute__((aligned(16))) float red[kEvenNW * 64 * (R <= 8 ? 4 : 1) * R];
     __shared__ float ssl[kEvenNW];
@@ -383,6 +402,15 @@ __global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe
         flat_pack_item<T, kEvenNT>(a.flat, int(blockIdx.x) - a.nwg);
         return;
     }
+#ifdef PSGD_EVEN_STAMPS
+    // diagnostic build: entry time, then the end of each of the first kEvenStamps - 2 segments
+    unsigned long long* const stp = a.stamps ? a.stamps + size_t(blockIdx.x) * kEvenStamps : nullptr;
+    if (stp && threadIdx.x == 0) {
+        stp[0] = __builtin_amdgcn_s_memrealtime();
+        stp[kEvenStamps - 1] = (uint64_t(uint32_t(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)))) << 32) |
+                               uint32_t(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
+    }
+#endif
     const int s0 = a.wg_seg[blockIdx.x], s1 = a.wg_seg[blockIdx.x + 1];
     if (s0 >= s1) return;
     // the next segment's descriptor and gradient pointer are loaded while this one streams
@@ -395,17 +423,20 @@ __global__ __launch_bounds__(kEvenNT) __attribute__((amdgpu_waves_per_eu(EvenWpe
             nx = a.segs[si + 1];
             ng = a.grads[nx.tensor];
         }
+        bool done = false;
         if constexpr (R <= 8) {
             if (sg.vec == 2) {
                 even_seg_full<T, R, K>(a, sg, gp, red, ssl);
-                continue;
-            }
-            if (sg.vec) {
+                done = true;
+            } else if (sg.vec) {
                 even_seg<T, R, K, 4>(a, sg, gp, red, ssl);
-                continue;
+                done = true;
             }
         }
-        even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+        if (!done) even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+#ifdef PSGD_EVEN_STAMPS
+        if (stp && threadIdx.x == 0 && si - s0 < kEvenStamps - 2) stp[1 + si - s0] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 

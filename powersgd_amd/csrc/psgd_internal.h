@@ -156,7 +156,11 @@ struct ProductArgs {
     const int32_t* wg_seg;
     int32_t nwg;
     FlatArgs flat;
+    // diagnostic builds only (-DPSGD_EVEN_STAMPS, tools/even_stamps.py): per workgroup of k_even
+    // kEvenStamps 64-bit words (s_memrealtime at entry and after each segment, the XCC / HW ids)
+    unsigned long long* stamps;
 };
+constexpr int kEvenStamps = 8;
 
 struct ApplyArgs {
     const MatDesc* mats;

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -459,6 +460,8 @@ struct psgd_plan {
     int32_t* xerr_dev = nullptr;
     bool xerr_set() const { return xerr_host && __atomic_load_n(xerr_host, __ATOMIC_ACQUIRE) != 0; }
     float* xout_now = nullptr;  // set per iteration by psgd_aggregate_ipc (exchange slot)
+    unsigned long long* stamp_buf = nullptr;  // diagnostic k_even stamps (PSGD_EVEN_STAMPS)
+    size_t stamp_words = 0;
     // history slot of the RAW in-factor the rank-1 norm fold reads: 1 (the local reduction's
     // output, world size 1) or 2 (the exchange's summed copy, psgd_aggregate_ipc)
     int raw_slot = 1;
@@ -490,6 +493,7 @@ struct psgd_plan {
             if (ipc_peer[w] && int(w) != ipc_rank) (void)hipIpcCloseMemHandle(ipc_peer[w]);
         if (ipc_buf) (void)hipFree(ipc_buf);  // peers must have closed it first (psgd_ipc_close)
         if (xerr_host) (void)hipHostFree(xerr_host);
+        if (stamp_buf) (void)hipFree(stamp_buf);
     }
 
     float* hist(int which, int k) const {  // 0: X (orthonormal in-factor), 1: Y local, 2: Y reduced
@@ -1396,6 +1400,51 @@ static int decompress_f64(psgd_plan* p, void* const* grads, void* out, int64_t s
     return PSGD_OK;
 }
 
+// Diagnostic (PSGD_EVEN_STAMPS=<file>, with a library built -DPSGD_EVEN_STAMPS): after every
+// k_even launch, synchronise and append its per-workgroup stamps to <file>: one line per launch,
+// "nwg", then per workgroup its segments' gradient bytes and the kEvenStamps words
+// (tools/even_stamps.py). Never set in a timed run.
+static int even_stamps_begin(psgd_plan* p, ProductArgs& pa) {
+    static const char* path = std::getenv("PSGD_EVEN_STAMPS");
+    if (!path || !*path) return PSGD_OK;
+    const size_t words = size_t(std::max(pa.nwg, 1)) * kEvenStamps;
+    if (p->stamp_words < words) {
+        if (p->stamp_buf) (void)hipFree(p->stamp_buf);
+        p->stamp_buf = nullptr;
+        PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->stamp_buf), words * sizeof(unsigned long long)));
+        p->stamp_words = words;
+    }
+    PSGD_HIP(hipMemset(p->stamp_buf, 0, words * sizeof(unsigned long long)));
+    pa.stamps = p->stamp_buf;
+    return PSGD_OK;
+}
+
+static int even_stamps_end(psgd_plan* p, const ProductArgs& pa, hipStream_t s) {
+    if (!pa.stamps) return PSGD_OK;
+    PSGD_HIP(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(size_t(pa.nwg) * kEvenStamps);
+    PSGD_HIP(hipMemcpy(h.data(), pa.stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    FILE* f = std::fopen(std::getenv("PSGD_EVEN_STAMPS"), "a");
+    if (!f) return PSGD_OK;
+    const int64_t esz = p->dtype == PSGD_BF16 ? 2 : 4;
+    const int32_t w0 = int32_t((pa.wg_seg - p->dev<int32_t>(p->o_wg_seg)));
+    std::fprintf(f, "%d", pa.nwg);
+    for (int w = 0; w < pa.nwg; ++w) {
+        int64_t bytes = 0;
+        const int32_t b = p->wg_seg[size_t(w0 + w)], e = p->wg_seg[size_t(w0 + w + 1)];
+        for (int32_t k = b; k < e; ++k) {
+            const Seg& sg = p->segs[size_t(k)];
+            const int64_t cols = std::min<int64_t>(int64_t(sg.lanes) * (sg.vec ? 4 : 1), sg.m - int64_t(sg.strip) * sg.lanes * (sg.vec ? 4 : 1));
+            bytes += int64_t(sg.row1 - sg.row0) * cols * esz;
+        }
+        std::fprintf(f, " %d:%lld", e - b, static_cast<long long>(bytes));
+        for (int k = 0; k < kEvenStamps; ++k) std::fprintf(f, ":%llu", h[size_t(w) * kEvenStamps + k]);
+    }
+    std::fprintf(f, "\n");
+    std::fclose(f);
+    return PSGD_OK;
+}
+
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
                          bool fuse, bool write_out, const FlatArgs* fl = nullptr,
                          const psgd_plan::Span* span = nullptr) {
@@ -1500,7 +1549,9 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         // world size > 1 (no output written here): the first iteration's launch also packs the
         // uncompressed tensors, ahead of every collective
         if (fl && !write_out && it == 0) pa.flat = *fl;
+        if (int st = even_stamps_begin(p, pa)) return st;
         PSGD_HIP(launch_even(p->dtype, p->rbucket, it, pa, pa.nwg, s));
+        if (int st = even_stamps_end(p, pa, s)) return st;
     } else {
         if (sp.ov[1] > sp.ov[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_ov) + sp.ov[0];

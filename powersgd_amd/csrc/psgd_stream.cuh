@@ -1078,7 +1078,10 @@ hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int nti
     // wider ranks load factor rows per element
     constexpr bool kCache = R <= 16;
     constexpr int kMaxNI = R <= 8 ? 4 : 2;
-    const int NI = (kCache && nterms <= kMaxNI) ? nterms : -1;
+    // world size > 1 (two term sets: local and all-reduced) caches fewer: the 4-term rank-4
+    // and rank-8 instances spilled VGPRs to scratch (tools/regs.py), the per-use loads do not
+    const int maxni = shared ? kMaxNI : (R <= 2 ? 4 : R == 4 ? 3 : 2);
+    const int NI = (kCache && nterms <= maxni) ? nterms : -1;
 #define PSGD_A(NN)                                                                       \
     do {                                                                                 \
         if (shared)                                                                      \
