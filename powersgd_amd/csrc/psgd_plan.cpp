@@ -309,7 +309,8 @@ thread_local const KernelTiming* g_kernel_timing = nullptr;
 // kEvenMinElems gradient elements per workgroup (small plans use fewer, fuller workgroups), at
 // most kMaxBuckets buckets (each bucket launch spreads over the whole chip).
 constexpr int kCUs = 256;                // MI355X
-constexpr int kEvenWgMax = 4 * kCUs;     // workgroups per launch (capacity)
+constexpr int kEvenWpcMax = 16;          // k_even workgroups per CU (PSGD_EVEN_WPC cap)
+constexpr int kEvenWgMax = kEvenWpcMax * kCUs;  // workgroups per launch (capacity)
 constexpr int kMaxBuckets = 8;
 
 struct psgd_plan {
@@ -344,6 +345,8 @@ struct psgd_plan {
     std::vector<Seg> segs;
     std::vector<int32_t> wg_seg;
     int even_wpc = 4;
+    int64_t even_segc = 4096;  // k_even cost model: elements-equivalent of one segment's fixed cost
+    int64_t even_skew = 0;     // k_even cost model: per-mille weight skew toward low block indices
     int64_t even_min = 16384;
     int even_order = 0;  // 0: each workgroup walks down strips; 1: row blocks across strips
     int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
@@ -611,11 +614,37 @@ struct psgd_plan {
                     }
                 }
             } else {
+                // Cost model (round 4, the per-workgroup stamps of profiles/r04/b): a workgroup's
+                // time is its gradient loads plus a fixed cost per segment (descriptor loads, a
+                // fresh load batch, the epilogue: ~1.5-2 us, i.e. even_segc elements at one
+                // workgroup's streaming rate), and a scalar-column strip (V = 1: 256 B per wave
+                // load instead of 1 KB) costs 4x per element. Equal COST ranges instead of equal
+                // bytes: the first workgroup used to take the five narrow segments of conv1 and the
+                // first 64-row matrices and finish last (22 us against p99 19 us).
+                const int64_t segc = even_segc;
+                auto rowc = [&](const MatDesc& d, int64_t cols) { return cols * (d.vec ? 1 : 4); };
+                int64_t totw = nwg * segc;
+                for (size_t i = m0; i < mi; ++i) {
+                    const MatDesc& d = mats[i];
+                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                    for (int s = 0; s < d.nstrip; ++s) totw += d.n * rowc(d, std::min<int64_t>(W, d.m - s * W)) + segc;
+                }
+                // Dispatch-order skew: at one round of resident workgroups the high block indices
+                // finish later for the same cost (profiles/r04/d: blocks 512-1023 p50 16-18 us,
+                // 0-511 12-13 us), so workgroup w gets weight 1 + skew (1 - 2 w / nwg)
+                const double sk = double(even_skew) / 1000.0;
+                const double wsum = double(nwg) * (1.0 + sk) - sk * double(nwg - 1);
+                auto wbound = [&](int64_t ww) {
+                    const double k = double(ww + 1);
+                    const double acc = k * (1.0 + sk) - sk * k * double(ww) / double(nwg);
+                    return ww + 1 >= nwg ? totw : int64_t(double(totw) * acc / wsum);
+                };
                 for (size_t i = m0; i < mi; ++i) {
                     const MatDesc& d = mats[i];
                     const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
                     for (int s = 0; s < d.nstrip; ++s) {
                         const int64_t cols = std::min<int64_t>(W, d.m - s * W);
+                        const int64_t rc = rowc(d, cols);
                         // k_even addresses a segment with 32-bit offsets: at most 2^30 bytes each
                         const int64_t es = dtype == PSGD_BF16 ? 2 : 4;
                         const int64_t seg_max = std::max<int64_t>(1, ((int64_t(1) << 30) / (d.m * es)) - 64);
@@ -623,7 +652,8 @@ struct psgd_plan {
                         while (r0 < d.n) {
                             int64_t take = std::min(d.n - r0, seg_max);
                             if (w < nwg - 1) {
-                                const int64_t fit = (bound(w) - cum + cols / 2) / cols;  // rows to this range's end
+                                // rows to this range's end, after paying the segment's fixed cost
+                                const int64_t fit = (wbound(w) - cum - segc + rc / 2) / rc;
                                 if (fit <= 0) {
                                     ++w;
                                     wg_seg.push_back(int32_t(segs.size()));
@@ -632,9 +662,9 @@ struct psgd_plan {
                                 take = std::min(take, fit);
                             }
                             make(i, s, r0, r0 + take);
-                            cum += take * cols;
+                            cum += segc + take * rc;
                             r0 += take;
-                            if (w < nwg - 1 && cum * nwg >= (w + 1) * total) {  // this range is full
+                            if (w < nwg - 1 && cum >= wbound(w)) {  // this range is full
                                 ++w;
                                 wg_seg.push_back(int32_t(segs.size()));
                             }
@@ -1030,9 +1060,11 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
                                  : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
         // persistent even product: workgroups per CU, minimum gradient elements per workgroup
-        p->even_wpc = int(std::min<int64_t>(4, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
+        p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
         p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
+        p->even_segc = std::max<int64_t>(0, env_int("PSGD_EVEN_SEGC", 4096));
+        p->even_skew = std::min<int64_t>(900, std::max<int64_t>(0, env_int("PSGD_EVEN_SKEW", 0)));
     }
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix
