@@ -239,11 +239,12 @@ def main():
     if world > 1 and not a.no_parity:
         # correctness of the cross-device run itself (after every timed block)
         out["multi_gpu_parity"] = multi_gpu_parity(world, rank, dev, backend)
+    if rank == 0 and world == 1:
+        # the real caller's cache state: autograd's accumulation into p.grad just before
+        out["post_backward"] = post_backward(a, a.config, dev)
     if rank == 0 and world == 1 and not a.no_extra:
         # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
         # world size 1, cold, same steps
-        # the real caller's cache state: autograd's accumulation into p.grad just before
-        out["post_backward"] = post_backward(a, a.config, dev)
         if a.config != "cfg3_resnet50_r4":
             r4 = measure(a, "cfg3_resnet50_r4", 1, 0, dev, backend, "cold")
             out["rank4"] = {k: r4[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}

@@ -56,14 +56,14 @@ __device__ __forceinline__ void fin_ld(rsrc_t rs, uint32_t e, bool ok, int32_t c
         for (int q = 0; q < 4; ++q) v[q] = BufIo<T>::ld1(rs, (ok && c + q < m) ? (e + q) * s : kOob);
     }
 }
-template <typename T, bool VEC>
+template <typename T, bool VEC, int AUX = PSGD_ST_AUX>
 __device__ __forceinline__ void fin_st(rsrc_t rs, uint32_t e, bool ok, int32_t c, int32_t m, const float (&v)[4]) {
     constexpr uint32_t s = sizeof(T);
     if constexpr (VEC) {
-        StIo<T>::st4(rs, ok ? e * s : kOob, v);
+        StIo<T>::template st4<AUX>(rs, ok ? e * s : kOob, v);
     } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) StIo<T>::st1(rs, (ok && c + q < m) ? (e + q) * s : kOob, v[q]);
+        for (int q = 0; q < 4; ++q) StIo<T>::template st1<AUX>(rs, (ok && c + q < m) ? (e + q) * s : kOob, v[q]);
     }
 }
 
@@ -387,7 +387,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                     }
                     const bool ok = valid && act[s];
                     fin_st<T, VEC>(gs, rowe + uint32_t(ccol[s]), ok, ccol[s], m, res);
-                    if (PJ || a.write_out) fin_st<T, VEC>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                    if (PJ || a.write_out) fin_st<T, VEC, PSGD_ST_AUX_OUT>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
                 }
             }
         }
@@ -482,7 +482,7 @@ __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& 
                 o[v] = o[v] + alpha * dotr<R>(aa, bb);
             }
         }
-        if (g.active) st_vec<T>(rO, uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T)), o);
+        if (g.active) st_vec<T, PSGD_ST_AUX_OUT>(rO, uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T)), o);
     }
 }
 

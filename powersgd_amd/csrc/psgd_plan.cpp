@@ -346,7 +346,6 @@ struct psgd_plan {
     std::vector<int32_t> wg_seg;
     int even_wpc = 4;
     int64_t even_segc = 4096;  // k_even cost model: elements-equivalent of one segment's fixed cost
-    int64_t even_skew = 0;     // k_even cost model: per-mille weight skew toward low block indices
     int64_t even_min = 16384;
     int even_order = 0;  // 0: each workgroup walks down strips; 1: row blocks across strips
     int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
@@ -629,16 +628,9 @@ struct psgd_plan {
                     const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
                     for (int s = 0; s < d.nstrip; ++s) totw += d.n * rowc(d, std::min<int64_t>(W, d.m - s * W)) + segc;
                 }
-                // Dispatch-order skew: at one round of resident workgroups the high block indices
-                // finish later for the same cost (profiles/r04/d: blocks 512-1023 p50 16-18 us,
-                // 0-511 12-13 us), so workgroup w gets weight 1 + skew (1 - 2 w / nwg)
-                const double sk = double(even_skew) / 1000.0;
-                const double wsum = double(nwg) * (1.0 + sk) - sk * double(nwg - 1);
-                auto wbound = [&](int64_t ww) {
-                    const double k = double(ww + 1);
-                    const double acc = k * (1.0 + sk) - sk * k * double(ww) / double(nwg);
-                    return ww + 1 >= nwg ? totw : int64_t(double(totw) * acc / wsum);
-                };
+                // (a dispatch-order skew, more cost to low block indices, was measured and does not
+                // help: the late blocks finish late whatever their share, profiles/r04/e)
+                auto wbound = [&](int64_t ww) { return ww + 1 >= nwg ? totw : (ww + 1) * totw / nwg; };
                 for (size_t i = m0; i < mi; ++i) {
                     const MatDesc& d = mats[i];
                     const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
@@ -1055,16 +1047,19 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         // elements per block.
         int64_t total = 0;
         for (auto& g : p->groups) total += int64_t(g.tensors.size()) * g.n * g.m;
+        // Rank 1 (256-thread row groups): twice as many, smaller blocks (ResNet-50: ~8k elements,
+        // ~3000 blocks): cfg2 0.0818 -> 0.0771 ms, final pass 55.7 -> 51.4 us; rank 4 (512-thread
+        // groups) slower there, 0.097 -> 0.103 ms (profiles/r04/g)
+        const int64_t per = maxr <= 1 ? 3072 : 1536;
         const int64_t dflt = total <= (int64_t(1) << 22)
                                  ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
-                                 : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
+                                 : std::min<int64_t>(65536, std::max<int64_t>(4096, total / per));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
         // persistent even product: workgroups per CU, minimum gradient elements per workgroup
         p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
         p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
         p->even_segc = std::max<int64_t>(0, env_int("PSGD_EVEN_SEGC", 4096));
-        p->even_skew = std::min<int64_t>(900, std::max<int64_t>(0, env_int("PSGD_EVEN_SKEW", 0)));
     }
 
     // output layout: dense, tensor order (what torch.cat / unflatten produce); a matrix

@@ -80,6 +80,13 @@ __device__ __forceinline__ void st_slot(float* p, float v) {
 #ifndef PSGD_ST_AUX
 #define PSGD_ST_AUX 19
 #endif
+// The output stores (the averaged gradient the optimizer reads next) take nt alone: measured
+// against sc0 | nt | sc1 (profiles/r04/g), cfg2 cold 0.0818 -> 0.0765-0.0772 ms, warm and
+// post-backward likewise faster, cfg3 unchanged; plain stores were between the two. The residual
+// (read again only after the next backward pass) keeps the write-through streaming policy.
+#ifndef PSGD_ST_AUX_OUT
+#define PSGD_ST_AUX_OUT 2
+#endif
 // A kernel launch that honours g_kernel_timing (psgd_internal.h)
 template <typename... Args>
 inline void timed_launch(void (*k)(Args...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
@@ -101,33 +108,41 @@ struct StIo;
 
 template <>
 struct StIo<float> {
+    template <int AUX = PSGD_ST_AUX>
     static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const v4u x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, PSGD_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, AUX);
     }
+    template <int AUX = PSGD_ST_AUX>
     static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, PSGD_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, AUX);
     }
 };
 
 template <>
 struct StIo<bf16_t> {
+    template <int AUX = PSGD_ST_AUX>
     static __device__ __forceinline__ void st4(rsrc_t r, uint32_t off, const float (&v)[4]) {
         typedef unsigned v2u_ __attribute__((ext_vector_type(2)));
         const v2u_ x = {uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16),
                         uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16)};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, PSGD_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, AUX);
     }
+    template <int AUX = PSGD_ST_AUX>
     static __device__ __forceinline__ void st1(rsrc_t r, uint32_t off, float v) {
-        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, PSGD_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, off, 0, AUX);
     }
 };
 // V consecutive elements at byte offset `off` of descriptor r
-template <typename T>
-__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[4]) { StIo<T>::st4(r, off, v); }
-template <typename T>
-__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[1]) { StIo<T>::st1(r, off, v[0]); }
+template <typename T, int AUX = PSGD_ST_AUX>
+__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[4]) {
+    StIo<T>::template st4<AUX>(r, off, v);
+}
+template <typename T, int AUX = PSGD_ST_AUX>
+__device__ __forceinline__ void st_vec(rsrc_t r, uint32_t off, const float (&v)[1]) {
+    StIo<T>::template st1<AUX>(r, off, v[0]);
+}
 
 template <typename T>
 struct Io;
@@ -1007,7 +1022,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
             if (g.active && row + u * g.stride < g.row_end) {
                 const uint32_t off = uint32_t((b.rc[u] - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
                 st_vec<T>(rD, off, b.x[u]);
-                st_vec<T>(rO, off, o);
+                st_vec<T, PSGD_ST_AUX_OUT>(rO, off, o);
             }
         }
     };
