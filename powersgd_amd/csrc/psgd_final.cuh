@@ -387,7 +387,12 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                     }
                     const bool ok = valid && act[s];
                     fin_st<T, VEC>(gs, rowe + uint32_t(ccol[s]), ok, ccol[s], m, res);
-                    if (PJ || a.write_out) fin_st<T, VEC, PSGD_ST_AUX_OUT>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                    if (PJ || a.write_out) {
+                        if (a.out_nt)
+                            fin_st<T, VEC, kStAuxOutNt>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                        else
+                            fin_st<T, VEC>(os, rowe + uint32_t(ccol[s]), ok, ccol[s], m, o);
+                    }
                 }
             }
         }
@@ -482,7 +487,13 @@ __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& 
                 o[v] = o[v] + alpha * dotr<R>(aa, bb);
             }
         }
-        if (g.active) st_vec<T, PSGD_ST_AUX_OUT>(rO, uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T)), o);
+        if (g.active) {
+            const uint32_t off = uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
+            if (a.out_nt)
+                st_vec<T, kStAuxOutNt>(rO, off, o);
+            else
+                st_vec<T>(rO, off, o);
+        }
     }
 }
 
@@ -534,18 +545,22 @@ hipError_t launch_final_k(const FinalArgs& a, int ntiles, hipStream_t s, int* wa
 template <typename T, int R, int SMAX>
 hipError_t dispatch_final_k(int nres, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     if (nres == kFinProj) return launch_final_k<T, R, SMAX, 0, true>(a, ntiles, s, waves);
-    switch (nres) {
-        case 0: return launch_final_k<T, R, SMAX, 0>(a, ntiles, s, waves);
-        case 1: return launch_final_k<T, R, SMAX, 1>(a, ntiles, s, waves);
-        case 2:
-            if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 2>(a, ntiles, s, waves);
-            break;
-        case 3:
-            if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 3>(a, ntiles, s, waves);
-            break;
-        default: break;
+    if constexpr (R == 4) {
+        return hipErrorInvalidValue;  // rank 4: the projection form only (psgd_plan.cpp, set_vec)
+    } else {
+        switch (nres) {
+            case 0: return launch_final_k<T, R, SMAX, 0>(a, ntiles, s, waves);
+            case 1: return launch_final_k<T, R, SMAX, 1>(a, ntiles, s, waves);
+            case 2:
+                if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 2>(a, ntiles, s, waves);
+                break;
+            case 3:
+                if constexpr (SMAX <= 3) return launch_final_k<T, R, SMAX, 3>(a, ntiles, s, waves);
+                break;
+            default: break;
+        }
+        return launch_final_k<T, R, SMAX, -1>(a, ntiles, s, waves);
     }
-    return launch_final_k<T, R, SMAX, -1>(a, ntiles, s, waves);
 }
 
 // Instantiated (R, SMAX) pairs: the ones that can keep two waves per SIMD without scratch

@@ -180,6 +180,7 @@ struct ApplyArgs {
     // buffer (psgd_reconstruct)
     void* const* rdst;
     void* const* odst;
+    int32_t out_nt;      // output stores nt only (large plans), else write-through (psgd_stream.cuh)
 };
 
 struct ReduceArgs {
@@ -255,6 +256,7 @@ struct FinalArgs {
     // items (ss_in), for ||Q_0,i||^2 of the matrix against the group norm
     const int32_t* mrng_in;
     float* xout;           // one-shot exchange: P local also to this rank's exchange slot, or null
+    int32_t out_nt;        // output stores nt only (large plans), else write-through (psgd_stream.cuh)
 };
 // nres value selecting the projection form of the fused final pass (I = 2, world size 1)
 constexpr int kFinProj = 1000;

@@ -339,6 +339,9 @@ struct psgd_plan {
     bool orth_chol = true;       // PSGD_ORTH_CHOL, read at set_vec (Cholesky-QR vs Householder)
     int fin_smax = 0;
     int64_t fin_elems = 32768, tiles_fin_cap = 0;
+    // output stores nt only (psgd_stream.cuh kStAuxOutNt): plans whose gradients exceed
+    // PSGD_OUT_NT_MB (default 32) MB; smaller plans keep the write-through policy
+    int32_t out_nt = 0;
     int64_t tiles_cap = 0, tiles_om_cap = 0;
     // even product (k_even): segments, per-workgroup segment ranges (wg_seg[w] .. wg_seg[w+1]),
     // workgroups per CU and the minimum elements per workgroup (read at create)
@@ -765,9 +768,10 @@ struct psgd_plan {
         tiles_ov.clear();
         tiles_om.clear();
         tiles_fin.clear();
-        // PSGD_FUSE_FINAL: 0 off; 1 (default) the K-term fused final at ranks 1-2; 2 also at
-        // rank 4 (it fits 512-thread rows but measured slower than the unfused kernels on
-        // ResNet-50, profiles/r01/sweep_final_lds.txt; correct, tests/test_gpu_final.py)
+        // PSGD_FUSE_FINAL: 0 off; 1 (default) the fused forms (K-term at ranks 1-2, projection at
+        // ranks 1/2/4). The rank-4 K-term form (two register panels: 253 VGPRs, one 512-thread
+        // workgroup per CU, profiles/r04/regs_final_f32.txt) measured 0.152 vs 0.119 ms for the
+        // unfused world-size > 1 step (profiles/r03/k) and is not built
         const int64_t fuse_mode = env_int("PSGD_FUSE_FINAL", 1);
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
@@ -825,7 +829,7 @@ struct psgd_plan {
                    launch_final_odd(dtype, rbucket, nres, fin_bucket(smax), none, 0, nullptr, &waves) == hipSuccess &&
                    waves >= 2;
         };
-        if (fuse_mode != 0 && small && (rbucket <= 2 || (rbucket == 4 && fuse_mode == 2))) fin_ok = fits(iters - 1);
+        if (fuse_mode != 0 && small && rbucket <= 2) fin_ok = fits(iters - 1);
         // Projection form (psgd_final.cuh): two power iterations at world size 1, ranks 2 and 4,
         // the last iteration's in-factor orthonormalised by Cholesky-QR (which leaves R').
         // Same register-panel geometry as the K-term form, so both can share the tile list.
@@ -1051,6 +1055,8 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         // ~3000 blocks): cfg2 0.0818 -> 0.0771 ms, final pass 55.7 -> 51.4 us; rank 4 (512-thread
         // groups) slower there, 0.097 -> 0.103 ms (profiles/r04/g)
         const int64_t per = maxr <= 1 ? 3072 : 1536;
+        const int64_t gbytes = total * (p->dtype == PSGD_BF16 ? 2 : p->dtype == PSGD_F64 ? 8 : 4);
+        p->out_nt = gbytes > env_int("PSGD_OUT_NT_MB", 32) * (int64_t(1) << 20) ? 1 : 0;
         const int64_t dflt = total <= (int64_t(1) << 22)
                                  ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
                                  : std::min<int64_t>(65536, std::max<int64_t>(4096, total / per));
@@ -1525,6 +1531,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     if (it == p->iters - 1 && p->fused_final(step, write_out)) {
         // last iteration, odd: product + residual (+ output at world size 1) in one pass
         FinalArgs fa{};
+        fa.out_nt = p->out_nt;
         fa.mats = p->dev<MatDesc>(p->o_mats);
         fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
         fa.grads = p->grad_tab.table();
@@ -1646,6 +1653,7 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     const int nt = sp.tiles[1] - sp.tiles[0];
     const int I = p->iters;
     ApplyArgs aa{};
+    aa.out_nt = p->out_nt;
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles) + sp.tiles[0];
     aa.grads = p->grad_tab.table();
@@ -1942,6 +1950,7 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
         if (int st = refresh_table(p, resid_out, p->rdst_tab, s)) return st;
     if (int st = refresh_table(p, out, p->odst_tab, s)) return st;
     ApplyArgs aa{};
+    aa.out_nt = p->out_nt;
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles);
     aa.grads = p->grad_tab.table();

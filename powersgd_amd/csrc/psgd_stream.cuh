@@ -80,13 +80,13 @@ __device__ __forceinline__ void st_slot(float* p, float v) {
 #ifndef PSGD_ST_AUX
 #define PSGD_ST_AUX 19
 #endif
-// The output stores (the averaged gradient the optimizer reads next) take nt alone: measured
-// against sc0 | nt | sc1 (profiles/r04/g), cfg2 cold 0.0818 -> 0.0765-0.0772 ms, warm and
-// post-backward likewise faster, cfg3 unchanged; plain stores were between the two. The residual
-// (read again only after the next backward pass) keeps the write-through streaming policy.
-#ifndef PSGD_ST_AUX_OUT
-#define PSGD_ST_AUX_OUT 2
-#endif
+// The output stores (the averaged gradient the optimizer reads next) of LARGE plans take nt
+// alone (ApplyArgs / FinalArgs::out_nt, chosen by the plan): measured against sc0 | nt | sc1
+// (profiles/r04/g, r04/h), cfg2 cold 0.082 -> 0.076 ms, warm and post-backward likewise faster,
+// cfg3 and cfg4 unchanged; the small plans (cfg1, cfg5: everything fits the Infinity Cache) were
+// 2-4 % slower with it and keep the write-through policy. Plain stores sat between the two. The
+// residual (read again only after the next backward pass) always streams write-through.
+constexpr int kStAuxOutNt = 2;
 // A kernel launch that honours g_kernel_timing (psgd_internal.h)
 template <typename... Args>
 inline void timed_launch(void (*k)(Args...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
@@ -1022,7 +1022,10 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
             if (g.active && row + u * g.stride < g.row_end) {
                 const uint32_t off = uint32_t((b.rc[u] - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
                 st_vec<T>(rD, off, b.x[u]);
-                st_vec<T, PSGD_ST_AUX_OUT>(rO, off, o);
+                if (a.out_nt)
+                    st_vec<T, kStAuxOutNt>(rO, off, o);
+                else
+                    st_vec<T>(rO, off, o);
             }
         }
     };

@@ -43,8 +43,7 @@ def _rel(a, b, scale):
 
 
 def _make(shapes, rank, iters, dtype=torch.float32, fuse=True, proj=True):
-    env = {"PSGD_FUSE_FINAL": ("2" if fuse is True else str(int(fuse))) if fuse else "0",  # 2 or 0
-           "PSGD_FIN_PROJ": "1" if proj else "0"}
+    env = {"PSGD_FUSE_FINAL": "1" if fuse else "0", "PSGD_FIN_PROJ": "1" if proj else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -64,17 +63,17 @@ def _make(shapes, rank, iters, dtype=torch.float32, fuse=True, proj=True):
 NARROW = [s for s in SHAPES if int(torch.tensor(s[1:]).prod()) <= 2048]
 
 
-# mode: PSGD_FUSE_FINAL for the fused plan (2: the K-term form allowed at every rank); "2k": mode
-# 2 with the projection form off (the K-term form at I = 2)
+# mode: "p" the default fused forms (projection form where it applies); "k": the projection form
+# off (the K-term form at I = 2, ranks 1-2; rank 4 has no K-term form and stays unfused)
 @pytest.mark.parametrize("rank,iters,narrow,mode", [
-    (1, 2, False, 2), (2, 2, False, 2), (1, 1, False, 2), (2, 1, False, 2), (1, 3, False, 2), (1, 4, False, 2),
-    (4, 2, False, 2), (2, 3, False, 2), (1, 3, True, 2), (2, 4, True, 2), (2, 2, True, 2),
-    (4, 2, False, "2k"), (2, 2, False, "2k"), (4, 2, True, 2), (4, 1, False, 2), (4, 1, True, 2)])
+    (1, 2, False, "p"), (2, 2, False, "p"), (1, 1, False, "p"), (2, 1, False, "p"), (1, 3, False, "p"),
+    (1, 4, False, "p"), (4, 2, False, "p"), (2, 3, False, "p"), (1, 3, True, "p"), (2, 4, True, "p"),
+    (2, 2, True, "p"), (4, 2, False, "k"), (2, 2, False, "k"), (4, 2, True, "p"), (4, 1, False, "p"),
+    (4, 1, True, "p")])
 def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
     shapes = NARROW if narrow else SHAPES
-    proj = mode != "2k"
-    mode = 2 if mode == "2k" else mode
-    fused = _make(shapes, rank, iters, fuse=mode, proj=proj)
+    proj = mode != "k"
+    fused = _make(shapes, rank, iters, fuse=True, proj=proj)
     plain = _make(shapes, rank, iters, fuse=False)
     plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
     plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
@@ -84,7 +83,7 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         form = fused._powersgd._plan.fused_final(t)
         n_fused += bool(form)
         if form:  # 2 = projection form: exactly the two-iteration rank-2/4 register-panel plans
-            assert (form == 2) == (proj and mode == 2 and iters == 2 and rank in (1, 2, 4)), (form, t)
+            assert (form == 2) == (proj and iters == 2 and rank in (1, 2, 4)), (form, t)
         ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 0.5, iters, 0)
         ora.codec.p_flat.copy_(fused._powersgd._ps_buffer.cpu())
         ora.codec.q_flat.copy_(fused._powersgd._qs_buffer.cpu())
@@ -110,8 +109,9 @@ def test_fused_final_vs_oracle_and_unfused(rank, iters, narrow, mode):
         plain._powersgd._ps_buffer.copy_(fused._powersgd._ps_buffer)
         plain._powersgd._qs_buffer.copy_(fused._powersgd._qs_buffer)
     expect_odd_last = sum(((t * iters + iters - 1) % 2) == 1 for t in range(3))
-    projection = proj and mode == 2 and iters == 2 and rank in (1, 2, 4)
-    if narrow or (rank == 1 and iters <= 2) or projection:  # configurations that must fuse
+    projection = proj and iters == 2 and rank in (1, 2, 4)
+    # configurations that must fuse (rank 4 fuses only in the projection form)
+    if (narrow and rank <= 2) or (rank == 1 and iters <= 2) or projection:
         assert n_fused == expect_odd_last, (n_fused, expect_odd_last)
 
 
