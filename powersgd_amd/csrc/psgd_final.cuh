@@ -489,10 +489,7 @@ __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& 
         }
         if (g.active) {
             const uint32_t off = uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
-            if (a.out_nt)
-                st_vec<T, kStAuxOutNt>(rO, off, o);
-            else
-                st_vec<T>(rO, off, o);
+            st_vec<T>(rO, off, o);
         }
     }
 }

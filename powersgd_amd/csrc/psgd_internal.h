@@ -180,7 +180,6 @@ struct ApplyArgs {
     // buffer (psgd_reconstruct)
     void* const* rdst;
     void* const* odst;
-    int32_t out_nt;      // output stores nt only (large plans), else write-through (psgd_stream.cuh)
 };
 
 struct ReduceArgs {

@@ -339,10 +339,9 @@ struct psgd_plan {
     bool orth_chol = true;       // PSGD_ORTH_CHOL, read at set_vec (Cholesky-QR vs Householder)
     int fin_smax = 0;
     int64_t fin_elems = 32768, tiles_fin_cap = 0;
-    // output stores nt only (psgd_stream.cuh kStAuxOutNt): plans whose gradients exceed
-    // PSGD_OUT_NT_MB (default 32) MB; smaller plans keep the write-through policy
+    // output stores of the fused final pass nt only (psgd_stream.cuh kStAuxOutNt): plans whose
+    // gradients exceed PSGD_OUT_NT_MB (default 32) MB; smaller plans keep the write-through policy
     int32_t out_nt = 0;
-    int32_t apply_nt = 0;  // the same for k_apply (the unfused residual + output pass)
     int64_t tiles_cap = 0, tiles_om_cap = 0;
     // even product (k_even): segments, per-workgroup segment ranges (wg_seg[w] .. wg_seg[w+1]),
     // workgroups per CU and the minimum elements per workgroup (read at create)
@@ -1058,7 +1057,6 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         const int64_t per = maxr <= 1 ? 3072 : 1536;
         const int64_t gbytes = total * (p->dtype == PSGD_BF16 ? 2 : p->dtype == PSGD_F64 ? 8 : 4);
         p->out_nt = gbytes > env_int("PSGD_OUT_NT_MB", 32) * (int64_t(1) << 20) ? 1 : 0;
-        p->apply_nt = p->out_nt && env_int("PSGD_APPLY_NT", 1) != 0 ? 1 : 0;
         const int64_t dflt = total <= (int64_t(1) << 22)
                                  ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
                                  : std::min<int64_t>(65536, std::max<int64_t>(4096, total / per));
@@ -1658,7 +1656,6 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     const int nt = sp.tiles[1] - sp.tiles[0];
     const int I = p->iters;
     ApplyArgs aa{};
-    aa.out_nt = p->apply_nt;
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles) + sp.tiles[0];
     aa.grads = p->grad_tab.table();
@@ -1955,7 +1952,6 @@ int psgd_reconstruct(psgd_plan* p, void* const* grads, void* const* resid_out, v
         if (int st = refresh_table(p, resid_out, p->rdst_tab, s)) return st;
     if (int st = refresh_table(p, out, p->odst_tab, s)) return st;
     ApplyArgs aa{};
-    aa.out_nt = p->apply_nt;
     aa.mats = p->dev<MatDesc>(p->o_mats);
     aa.tiles = p->dev<Tile>(p->o_tiles);
     aa.grads = p->grad_tab.table();

@@ -253,6 +253,46 @@ __device__ void orth_joint_norm(const OrthArgs& a, const OrthUnit& u, double* rd
     const int tid = threadIdx.x;
     constexpr int U = 8;
     float part = 0.f;
+    // a group of at most U1 * NT values (every rank-1 group of cfg2 at W > 1): all loads in
+    // one round trip, no second pass; the per-thread order of the sums is the batched loop's
+    constexpr int U1 = 16;
+    if (total <= int64_t(U1) * NT) {
+        float x[U1];
+#pragma unroll
+        for (int q = 0; q < U1; ++q) {  // unconditional loads from clamped indices (no branches)
+            const int64_t i = tid + int64_t(q) * NT;
+            x[q] = st[i < total ? i : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < U1; ++q) {
+            const int64_t i = tid + int64_t(q) * NT;
+            keep(x[q]);
+            x[q] = i < total ? x[q] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < U1; ++q) part = fmaf(x[q], x[q], part);
+        double s = wave_allsum(part);
+        if ((tid & 63) == 0) rd[tid >> 6] = s;
+        __syncthreads();
+        s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += rd[w];
+        const float nrm = float(sqrt(s));
+        const float d = nrm > 1e-16f ? nrm : 1e-16f;
+        if (a.rfac)
+            for (int c = tid; c < u.count; c += NT) a.rfac[u.off + int64_t(c) * u.k] = d;
+#pragma unroll
+        for (int q = 0; q < U1; ++q) {
+            const int64_t i = tid + int64_t(q) * NT;
+            if (i < total) {
+                if (sv) sv[i] = x[q];
+                const float y = x[q] / d;
+                st[i] = y;
+                hx[i] = y;
+            }
+        }
+        return;
+    }
     for (int64_t base = tid; base < total; base += int64_t(U) * NT) {
         float x[U];
 #pragma unroll

@@ -80,12 +80,15 @@ __device__ __forceinline__ void st_slot(float* p, float v) {
 #ifndef PSGD_ST_AUX
 #define PSGD_ST_AUX 19
 #endif
-// The output stores (the averaged gradient the optimizer reads next) of LARGE plans take nt
-// alone (ApplyArgs / FinalArgs::out_nt, chosen by the plan): measured against sc0 | nt | sc1
-// (profiles/r04/g, r04/h), cfg2 cold 0.082 -> 0.076 ms, warm and post-backward likewise faster,
-// cfg3 and cfg4 unchanged; the small plans (cfg1, cfg5: everything fits the Infinity Cache) were
-// 2-4 % slower with it and keep the write-through policy. Plain stores sat between the two. The
-// residual (read again only after the next backward pass) always streams write-through.
+// The output stores (the averaged gradient the optimizer reads next) of the fused world-size-1
+// final pass of LARGE plans take nt alone (FinalArgs::out_nt, chosen by the plan): measured
+// against sc0 | nt | sc1 (profiles/r04/g, r04/h), cfg2 cold 0.082 -> 0.076 ms, warm and
+// post-backward likewise faster, cfg3 and cfg4 unchanged; the small plans (cfg1, cfg5:
+// everything fits the Infinity Cache) were 2-4 % slower with it and keep the write-through
+// policy. Plain stores sat between the two. The residual (read again only after the next
+// backward pass) always streams write-through, and so do k_apply and k_lowrank_out: nt made the
+// write-only k_lowrank_out slower (19.6 -> 23.0 us, cfg2 W > 1), and k_apply's run-time choice
+// cost a wave per SIMD of occupancy for no measured gain (profiles/r04/o).
 constexpr int kStAuxOutNt = 2;
 // A kernel launch that honours g_kernel_timing (psgd_internal.h)
 template <typename... Args>
@@ -1022,10 +1025,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
             if (g.active && row + u * g.stride < g.row_end) {
                 const uint32_t off = uint32_t((b.rc[u] - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
                 st_vec<T>(rD, off, b.x[u]);
-                if (a.out_nt)
-                    st_vec<T, kStAuxOutNt>(rO, off, o);
-                else
-                    st_vec<T>(rO, off, o);
+                st_vec<T>(rO, off, o);
             }
         }
     };

@@ -16,4 +16,10 @@ a = argparse.Namespace(steps=int(os.environ.get("AB_STEPS", "100")), warmup=10, 
 dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 r = bench.one_rank_group(a, dev)
-print(json.dumps({k: (v["ms_per_step"] if isinstance(v, dict) else v) for k, v in r.items() if k != "note"}))
+def ms(v):
+    if not isinstance(v, dict):
+        return v
+    return v["ms_per_step"] if "ms_per_step" in v else {k: ms(x) for k, x in v.items()}
+
+
+print(json.dumps({k: ms(v) for k, v in r.items() if k != "note"}))
