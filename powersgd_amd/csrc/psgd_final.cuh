@@ -92,8 +92,9 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rg = tid / Tg, tt = tid - rg * Tg;
     const int RGS = NT / Tg;
-    const int64_t row0 = int64_t(t.chunk) * d.fin_rows;
-    const int64_t row_end = d.n < row0 + d.fin_rows ? d.n : row0 + d.fin_rows;
+    const int64_t frows = PJ ? d.fin_rows : d.fin_rows_kt;
+    const int64_t row0 = int64_t(t.chunk) * frows;
+    const int64_t row_end = d.n < row0 + frows ? d.n : row0 + frows;
     const int nres = K >= 0 ? K : a.nres;
     const uint32_t nbytes = uint32_t(d.n * d.m * int64_t(sizeof(T)));
     const rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.grads[t.tensor], 0, int(nbytes), 0x00020000);

@@ -51,11 +51,12 @@ struct MatDesc {
     int32_t odd_sw;         // MFMA strip width (columns, multiple of 16)
     int32_t odd_chunk_rows; // MFMA chunk rows (multiple of 16 * kWaves)
     // fused final odd iteration (k_final_odd): a row group of fin_T threads owns a row
-    // (fin_S segments of 4*fin_T columns); a workgroup covers fin_rows rows
+    // (fin_S segments of 4*fin_T columns); a workgroup covers fin_rows rows in the projection
+    // form, fin_rows_kt in the K-term form
     int32_t fin_T;
     int32_t fin_S;
     int32_t fin_rows;
-    int32_t fin_pad;
+    int32_t fin_rows_kt;
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.

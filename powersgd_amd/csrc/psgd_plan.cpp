@@ -334,11 +334,15 @@ struct psgd_plan {
     std::vector<Tile> tiles_ov;  // lane-column tiles of the odd-VALU matrices
     std::vector<Tile> tiles_om;  // MFMA tiles of the odd-MFMA matrices
     std::vector<Tile> tiles_fin; // row blocks of the fused final odd pass
+    // the K-term form's own row blocks when they differ from the projection form's (MatDesc::
+    // fin_rows_kt); empty: the K-term form uses tiles_fin
+    std::vector<Tile> tiles_fin_kt;
     bool fin_ok = false;         // every matrix fits the fused final odd pass (K-term form)
     bool fin_proj = false;       // ... in its projection form (I = 2, psgd_aggregate only)
     bool orth_chol = true;       // PSGD_ORTH_CHOL, read at set_vec (Cholesky-QR vs Householder)
     int fin_smax = 0;
     int64_t fin_elems = 32768, tiles_fin_cap = 0;
+    int64_t fin_elems_kt = 32768, tiles_fin_kt_cap = 0;
     // output stores of the fused final pass nt only (psgd_stream.cuh kStAuxOutNt): plans whose
     // gradients exceed PSGD_OUT_NT_MB (default 32) MB; smaller plans keep the write-through policy
     int32_t out_nt = 0;
@@ -363,7 +367,7 @@ struct psgd_plan {
     int64_t panel_p = 0, panel_q = 0;
     int64_t part_odd_floats = 0;  // odd partials [odd strips][n][r] per matrix; even ones follow
     double unc_floats = 0, comp_floats = 0;
-    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_tiles_fin = 0, o_red_even = 0,
+    size_t o_ptrs = 0, o_mats = 0, o_tiles = 0, o_tiles_ov = 0, o_tiles_om = 0, o_tiles_fin = 0, o_tiles_fin_kt = 0, o_red_even = 0,
            o_red_odd = 0, o_units_p = 0, o_units_q = 0, o_hist = 0, o_part = 0, o_grng_even = 0,
            o_grng_odd = 0, o_ss = 0, ss_stride = 0, o_ss0 = 0, o_grng_ss0 = 0, o_segs = 0, o_wg_seg = 0,
            ws_bytes = 0;
@@ -373,7 +377,7 @@ struct psgd_plan {
     // Buckets of whole shape groups (W > 1 overlap, psgd_plan_set_buckets): per bucket the
     // [begin, end) range of every launch list (all are in matrix order) and of the P/Q buffers.
     struct Span {
-        int32_t tiles[2], ov[2], om[2], fin[2], re[2], ro[2], up[2], uq[2], wg[2];
+        int32_t tiles[2], ov[2], om[2], fin[2], fin_kt[2], re[2], ro[2], up[2], uq[2], wg[2];
         int64_t p[2], q[2];
     };
     std::vector<int32_t> bucket_gend;              // exclusive group end per bucket
@@ -386,6 +390,7 @@ struct psgd_plan {
         sp.ov[1] = int32_t(tiles_ov.size());
         sp.om[1] = int32_t(tiles_om.size());
         sp.fin[1] = int32_t(tiles_fin.size());
+        sp.fin_kt[1] = int32_t(tiles_fin_kt.size());
         sp.re[1] = int32_t(red_even.size());
         sp.ro[1] = int32_t(red_odd.size());
         sp.up[1] = int32_t(units_p.size());
@@ -418,6 +423,7 @@ struct psgd_plan {
             range(tiles_ov, tk, sp.ov);
             range(tiles_om, tk, sp.om);
             range(tiles_fin, tk, sp.fin);
+            range(tiles_fin_kt, tk, sp.fin_kt);
             range(red_even, rk, sp.re);
             range(red_odd, rk, sp.ro);
             range(unit_group_p, [&](int32_t g) { return g >= g0 && g < g1; }, sp.up);
@@ -768,6 +774,7 @@ struct psgd_plan {
         tiles_ov.clear();
         tiles_om.clear();
         tiles_fin.clear();
+        tiles_fin_kt.clear();
         // PSGD_FUSE_FINAL: 0 off; 1 (default) the fused forms (K-term at ranks 1-2, projection at
         // ranks 1/2/4). The rank-4 K-term form (two register panels: 253 VGPRs, one 512-thread
         // workgroup per CU, profiles/r04/regs_final_f32.txt) measured 0.152 vs 0.119 ms for the
@@ -844,14 +851,25 @@ struct psgd_plan {
             // segments per row up to the kernel bucket the widest groups already need
             // (at most 5: the exact-S bodies), for fewer idle lanes
             const int scap = env_int("PSGD_FIN_GEOM", 1) ? std::min(fin_bucket(smax), 5) : 0;
+            // row blocks: the projection form's fin_elems; the K-term form's fin_elems_kt (its own
+            // list only when both forms exist and the sizes differ; fin_rows_kt = fin_rows else)
+            const int64_t fe = fin_proj ? fin_elems : fin_elems_kt;
+            const bool two = fin_proj && fin_ok && fin_elems_kt != fin_elems;
             for (size_t i = 0; i < mats.size(); ++i) {
                 MatDesc& d = mats[i];
-                const FinGeom fg = fin_geometry(d.n, d.m, rbucket, fin_elems, scap);
+                const FinGeom fg = fin_geometry(d.n, d.m, rbucket, fe, scap);
                 d.fin_T = fg.T;
                 d.fin_S = fg.S;
                 d.fin_rows = fg.rows;
+                d.fin_rows_kt = fg.rows;
                 fin_smax = std::max(fin_smax, fg.S);
                 for (int64_t b = 0; b < fg.ntiles; ++b) tiles_fin.push_back(Tile{int32_t(i), 0, int32_t(b), d.tensor});
+                if (two) {
+                    const FinGeom fk = fin_geometry(d.n, d.m, rbucket, fin_elems_kt, scap);
+                    d.fin_rows_kt = fk.rows;
+                    for (int64_t b = 0; b < fk.ntiles; ++b)
+                        tiles_fin_kt.push_back(Tile{int32_t(i), 0, int32_t(b), d.tensor});
+                }
             }
         }
         build_reduction();
@@ -916,12 +934,14 @@ int refresh_pointers(psgd_plan* p, void* const* grads, hipStream_t stream) {
 int psgd_plan::upload_tiles() const {
     // the lists follow the geometry and the buckets: never past the capacities carved at create
     if (int64_t(segs.size()) > segs_cap || int64_t(wg_seg.size()) > int64_t(kMaxBuckets) * kEvenWgMax + 1 ||
-        int64_t(red_even.size()) > red_even_cap || int64_t(red_odd.size()) > red_odd_cap)
+        int64_t(red_even.size()) > red_even_cap || int64_t(red_odd.size()) > red_odd_cap ||
+        int64_t(tiles_fin.size()) > tiles_fin_cap || int64_t(tiles_fin_kt.size()) > tiles_fin_kt_cap)
         return fail(PSGD_ERR_STATE, "internal: work lists exceed their workspace capacity");
     if (int st = upload(dev<void>(o_mats), mats.data(), mats.size() * sizeof(MatDesc))) return st;
     if (int st = upload(dev<void>(o_tiles), tiles.data(), tiles.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_ov), tiles_ov.data(), tiles_ov.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_fin), tiles_fin.data(), tiles_fin.size() * sizeof(Tile))) return st;
+    if (int st = upload(dev<void>(o_tiles_fin_kt), tiles_fin_kt.data(), tiles_fin_kt.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_tiles_om), tiles_om.data(), tiles_om.size() * sizeof(Tile))) return st;
     if (int st = upload(dev<void>(o_segs), segs.data(), segs.size() * sizeof(Seg))) return st;
     if (int st = upload(dev<void>(o_wg_seg), wg_seg.data(), wg_seg.size() * sizeof(int32_t))) return st;
@@ -1061,6 +1081,12 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
                                  ? std::min<int64_t>(16384, std::max<int64_t>(4096, total / 256))
                                  : std::min<int64_t>(65536, std::max<int64_t>(4096, total / per));
         p->fin_elems = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS", dflt));
+        // the K-term form (world size > 1, and world size 1 beyond two iterations) keeps ~16k at
+        // every rank: cfg2 over the multi-GPU code path 0.0932-0.0959 -> 0.0916-0.0918 ms
+        // (profiles/r04/o)
+        const int64_t dflt_kt = total <= (int64_t(1) << 22) ? dflt
+                                                            : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
+        p->fin_elems_kt = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS_KT", env_int("PSGD_FIN_ELEMS", dflt_kt)));
         // persistent even product: workgroups per CU, minimum gradient elements per workgroup
         p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
@@ -1141,10 +1167,13 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->tiles_cap += std::max(geometry(md.n, md.m, md.r, p->base_vec[i], p->tile_elems).ntiles,
                                  geometry(md.n, md.m, md.r, 0, p->tile_elems).ntiles);
         p->tiles_om_cap += int64_t(og.nstrip) * og.nchunk;
-        int64_t cap = 0;
-        for (int sc = 0; sc <= 5; ++sc)  // any segment cap set_vec may pick
+        int64_t cap = 0, cap_kt = 0;
+        for (int sc = 0; sc <= 5; ++sc) {  // any segment cap set_vec may pick
+            cap_kt = std::max(cap_kt, fin_geometry(md.n, md.m, p->rbucket, p->fin_elems_kt, sc).ntiles);
             cap = std::max(cap, fin_geometry(md.n, md.m, p->rbucket, p->fin_elems, sc).ntiles);
-        p->tiles_fin_cap += cap;
+        }
+        p->tiles_fin_cap += std::max(cap, cap_kt);
+        p->tiles_fin_kt_cap += cap_kt;
         strips_max += ns;
         strip_elems += se;
         red_even_cap += re;
@@ -1187,6 +1216,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_tiles_ov = carve(size_t(p->tiles_cap) * sizeof(Tile));
     p->o_tiles_om = carve(size_t(std::max<int64_t>(p->tiles_om_cap, 1)) * sizeof(Tile));
     p->o_tiles_fin = carve(size_t(std::max<int64_t>(p->tiles_fin_cap, 1)) * sizeof(Tile));
+    p->o_tiles_fin_kt = carve(size_t(std::max<int64_t>(p->tiles_fin_kt_cap, 1)) * sizeof(Tile));
     p->o_segs = carve(size_t(std::max<int64_t>(p->segs_cap, 1)) * sizeof(Seg));
     p->o_wg_seg = carve((size_t(kMaxBuckets) * kEvenWgMax + 1) * sizeof(int32_t));
     p->o_red_even = carve(size_t(std::max<int64_t>(p->red_even_cap, 1)) * sizeof(RedItem));
@@ -1536,7 +1566,10 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         FinalArgs fa{};
         fa.out_nt = p->out_nt;
         fa.mats = p->dev<MatDesc>(p->o_mats);
-        fa.tiles = p->dev<Tile>(p->o_tiles_fin) + sp.fin[0];
+        // the K-term form on its own row blocks when the plan has them (MatDesc::fin_rows_kt)
+        const bool own_kt = !proj && !p->tiles_fin_kt.empty();
+        const int32_t(&fr)[2] = own_kt ? sp.fin_kt : sp.fin;
+        fa.tiles = p->dev<Tile>(own_kt ? p->o_tiles_fin_kt : p->o_tiles_fin) + fr[0];
         fa.grads = p->grad_tab.table();
         fa.out = p->out_now;
         fa.x = fused ? p->hist(p->raw_slot, it - 1) : p->hist(0, it);
@@ -1552,7 +1585,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
             fa.xstate = in;
             fa.hx = p->hist(0, it);
         }
-        const int nfin = sp.fin[1] - sp.fin[0];
+        const int nfin = fr[1] - fr[0];
         if (proj) {  // no error-feedback terms: P_0 and R' only (rank 1: P_0 and the matrix's c)
             fa.proj_p0 = p->hist(0, 0);
             fa.proj_r = p->dev<float>(p->o_rq);
