@@ -450,7 +450,13 @@ __global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu
 }
 
 // output = sum_k alpha * (A_k B_k^T) on the lane-column tiles (same order as k_apply's
-// output term, reference :211-219)
+// output term, reference :211-219). kLowrankUR rows per lane in flight: cfg2 over the
+// multi-GPU code path 21.1 -> 20.4 us (profiles/r04/r; the write-only ceiling of the same
+// bytes is ~17.9 us, profiles/r04/q)
+#ifndef PSGD_LOWRANK_UR
+#define PSGD_LOWRANK_UR 4
+#endif
+constexpr int kLowrankUR = PSGD_LOWRANK_UR;
 template <typename T, int R, int NI, int V>
 __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
     const TileGeom g = tile_geom<V>(d, t);
@@ -468,6 +474,36 @@ __device__ __forceinline__ void lowrank_tile(const ApplyArgs& a, const MatDesc& 
                 ld_factor<R>(gconst<float>(a.apx.q[k]) + d.qoff + (g.ccol + v) * r, r, ba[k][v]);
     }
     const float alpha = a.alpha;
+    if constexpr (NI > 0 && kLowrankUR > 1) {
+        // kLowrankUR rows per lane in flight: their P-factor loads first, then the stores (the
+        // same per-element arithmetic and order as the loop below)
+        for (int64_t row0 = g.first_row; row0 < g.row_end; row0 += int64_t(kLowrankUR) * g.stride) {
+            float pa[kLowrankUR][NI][R];
+#pragma unroll
+            for (int u = 0; u < kLowrankUR; ++u) {
+                const int64_t row = row0 + int64_t(u) * g.stride;
+                const int32_t prow = int32_t(row < g.row_end ? row : row0) * r;
+#pragma unroll
+                for (int k = 0; k < NI; ++k) ld_factor<R>(gconst<float>(a.apx.p[k]) + d.poff + prow, r, pa[u][k]);
+            }
+#pragma unroll
+            for (int u = 0; u < kLowrankUR; ++u) {
+                const int64_t row = row0 + int64_t(u) * g.stride;
+                float o[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) o[v] = 0.f;
+#pragma unroll
+                for (int k = 0; k < NI; ++k)
+#pragma unroll
+                    for (int v = 0; v < V; ++v) o[v] = o[v] + alpha * dotr<R>(pa[u][k], ba[k][v]);
+                if (g.active && row < g.row_end) {
+                    const uint32_t off = uint32_t((row - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
+                    st_vec<T>(rO, off, o);
+                }
+            }
+        }
+        return;
+    }
     for (int64_t row = g.first_row; row < g.row_end; row += g.stride) {
         const int32_t prow = int32_t(row) * r;
         float o[V];
