@@ -1113,6 +1113,16 @@ __device__ __forceinline__ void chol_chain(const double* g, const float* top, co
         }
 }
 
+// rows per thread per load batch of k_orth_chol (ranks 2 / 4). Larger batches (fewer round
+// trips on long panels) measured slower: 16 / 12 rows, k_orth_chol<2> 8.5 -> 9.5 us (cfg4),
+// <4> 6.3 -> 6.8 us (profiles/r04/t); likewise the whole panel held in registers (r04/l)
+#ifndef PSGD_CHOL_U2
+#define PSGD_CHOL_U2 8
+#endif
+#ifndef PSGD_CHOL_U4
+#define PSGD_CHOL_U4 8
+#endif
+
 // Gram sums through LDS (NT x NG fp64 partials: 40 KB at rank 4) for r <= 4
 template <int R>
 constexpr bool kGramLds = R <= 4;
@@ -1132,7 +1142,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     // rows in batches of kU per thread, all loads of a batch issued together (clamped
     // rows, masked afterwards): the panel was just written by another kernel, so each
     // batch costs one L2/MALL round trip rather than one per row
-    constexpr int kU = R <= 4 ? 8 : 4;
+    constexpr int kU = R <= 2 ? PSGD_CHOL_U2 : R <= 4 ? PSGD_CHOL_U4 : 4;
     double g[NG];
 #pragma unroll
     for (int e = 0; e < NG; ++e) g[e] = 0.0;
