@@ -19,8 +19,9 @@ def _rel(a, b, scale):
     return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
 
 
-def _worker(_, port, cfg, steps, buckets=1):
+def _worker(_, port, cfg, steps, buckets=1, env=None):
     os.environ["PSGD_COMM_BUCKETS"] = str(buckets)
+    os.environ.update(env or {})  # plan knobs, read at plan creation
     from oracle import powersgd_oracle as O
     from powersgd_amd import Config, PowerSGD, _lib
     from powersgd_amd.workloads import CONFIGS, hash_tensors
@@ -79,3 +80,14 @@ def test_rccl_bucketed_overlap_vs_oracle(cfg):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     torch.multiprocessing.spawn(_worker, args=(port, cfg, 3, 4), nprocs=1, join=True)
+
+
+def test_rccl_kterm_own_row_blocks_vs_oracle():
+    """The K-term final pass on its own row blocks (psgd_plan.cpp tiles_fin_kt, MatDesc::
+    fin_rows_kt) at an odd block size, 5000 elements: ragged against every ResNet-50 row length,
+    beside the projection form's default blocks of the same plan."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    torch.multiprocessing.spawn(_worker, args=(port, "cfg2_resnet50_r1", 2, 1, {"PSGD_FIN_ELEMS_KT": "5000"}),
+                                nprocs=1, join=True)
