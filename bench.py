@@ -59,7 +59,7 @@ def parse():
                     help="profiling runs: time only one cache state (the headline needs 'both' or 'cold')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N = 1: skip the rank-4 block and the world-size > 1 path block (1-rank RCCL group)")
+                    help="skip the rank4/cfg4/cfg5 blocks and (N = 1) the world-size > 1 path block")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-parity", action="store_true",
                     help="N > 1: skip the cross-GPU parity check of the W > 1 transports (after the timed blocks)")
@@ -236,20 +236,27 @@ def main():
     if world > 1 and backend == "nccl" and "PSGD_COMM_BUCKETS" not in os.environ:
         # the RCCL step with 2 buckets: each bucket's collective under the next bucket's kernels
         out["rccl_buckets2"] = env_block(a, world, rank, dev, backend, {"PSGD_COMM_BUCKETS": "2"})
-    if world > 1 and not a.no_parity:
-        # correctness of the cross-device run itself (after every timed block)
-        out["multi_gpu_parity"] = multi_gpu_parity(world, rank, dev, backend)
     if rank == 0 and world == 1:
         # the real caller's cache state: autograd's accumulation into p.grad just before
         out["post_backward"] = post_backward(a, a.config, dev)
+    if not a.no_extra:
+        # every other config BASELINE names for this run, at this world size (cold, same steps):
+        # rank4 = cfg3, the north-star ResNet-50 rank-4 config ("rank=1/4 ... at 1 and 8 GPUs");
+        # cfg4 = the bf16 Llama linears; cfg5 = the LSTM matrix at four power iterations (four
+        # collectives per step at N > 1). All ranks take part (collective timing at N > 1).
+        for key, cfg in EXTRA_BLOCKS:
+            if cfg == a.config:
+                continue
+            m = measure(a, cfg, world, rank, dev, backend, "cold")
+            keep = ("value", "ms_per_step", "per_rank_GBs", "roofline", "step_roofline")
+            out[key] = {k: m[k] for k in keep if key == "rank4" or k != "roofline"}
+            out[key]["config"] = m["config"]
+            if rank == 0 and world == 1 and key == "rank4":
+                out[key]["post_backward"] = post_backward(a, cfg, dev)
+    if world > 1 and not a.no_parity:
+        # correctness of the cross-device run itself (after every timed block)
+        out["multi_gpu_parity"] = multi_gpu_parity(world, rank, dev, backend)
     if rank == 0 and world == 1 and not a.no_extra:
-        # the other half of the metric ("rank=1/4"): the north-star ResNet-50 rank-4 config at
-        # world size 1, cold, same steps
-        if a.config != "cfg3_resnet50_r4":
-            r4 = measure(a, "cfg3_resnet50_r4", 1, 0, dev, backend, "cold")
-            out["rank4"] = {k: r4[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
-            out["rank4"]["config"] = r4["config"]
-            out["rank4"]["post_backward"] = post_backward(a, "cfg3_resnet50_r4", dev)
         # the world-size > 1 code path (bucketed async factor all-reduces, per-bucket kernels,
         # write-only output pass) timed on this one GPU through a 1-rank RCCL group: the
         # per-rank compute floor of every multi-GPU point (no xGMI traffic: one rank)
@@ -269,6 +276,9 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+EXTRA_BLOCKS = (("rank4", "cfg3_resnet50_r4"), ("cfg4", "cfg4_llama_r2_bf16"), ("cfg5", "cfg5_lstm_r1_i4"))
+
+
 def CONFIGS_():
     from powersgd_amd.workloads import CONFIGS
 
@@ -283,8 +293,11 @@ def CONFIGS_():
 # reference, W threads meeting at the reference's SUM all-reduce, powersgd.py:204-219). The
 # oracle is the checker here, never the thing measured.
 PARITY_STEPS = 2
-PARITY_CFGS = ("cfg2_resnet50_r1", "cfg3_resnet50_r4")
-PARITY_TOL = (1e-5, 1e-4)  # step 0 (same state), step 1 (free-running)
+# every config BASELINE names for the multi-GPU runs (cfg3: rank 4; cfg4: bf16 with 11008-column
+# rows; cfg5: four power iterations, i.e. four collectives per step) and the headline cfg2
+PARITY_CFGS = ("cfg2_resnet50_r1", "cfg3_resnet50_r4", "cfg4_llama_r2_bf16", "cfg5_lstm_r1_i4")
+PARITY_TOL = (1e-5, 1e-4)  # fp32: step 0 (same state), step 1 (free-running)
+PARITY_TOL_BF16 = (4e-3, 4e-3)  # bf16 gradient storage (the residual is stored in bf16)
 
 
 def parity_inputs(shapes, rank, t):
@@ -305,17 +318,18 @@ def gather_to_rank0(t, world, rank, backend):
     return parts
 
 
-def parity_collect(step, shapes, world, rank, backend, dev):
+def parity_collect(step, shapes, world, rank, backend, dev, dtype=torch.float32):
     """PARITY_STEPS steps of `step(grads) -> outs` on this rank (error feedback: the residual
-    left in `grads` + the next fresh gradient), then the gathers. Every rank makes the same
-    collectives even if its steps failed (its rows are NaN then), so a failure cannot hang the
-    others. Returns (outs[t][w], residuals[t][w], errors[w]) on rank 0."""
+    left in `grads` + the next fresh gradient, added in fp32 and stored in `dtype`), then the
+    gathers. Every rank makes the same collectives even if its steps failed (its rows are NaN
+    then), so a failure cannot hang the others. Returns (outs[t][w], residuals[t][w], errors[w])
+    on rank 0."""
     total = sum(numel(s) for s in shapes)
     flats, err = [], None
     try:
-        res = [torch.zeros(s, device=dev) for s in shapes]
+        res = [torch.zeros(s, device=dev, dtype=dtype) for s in shapes]
         for t in range(PARITY_STEPS):
-            g = [r + x.to(dev) for r, x in zip(res, parity_inputs(shapes, rank, t))]
+            g = [(r.float() + x.to(dev)).to(dtype) for r, x in zip(res, parity_inputs(shapes, rank, t))]
             o = step(g)
             flats.append((torch.cat([x.reshape(-1).float() for x in o]), torch.cat([x.reshape(-1).float() for x in g])))
             res = g
@@ -333,12 +347,16 @@ def parity_collect(step, shapes, world, rank, backend, dev):
 
 def parity_check(c, world, p0, q0, outs, ress):
     """Rank 0: the reference's W-worker steps on the same inputs from the same P/Q state; the
-    largest per-tensor error relative to that rank's input tensor (SURVEY §8(c) metric)."""
+    largest per-tensor error relative to that rank's input tensor (SURVEY §8(c) metric). bf16
+    configs: each worker's input is exactly the device's (its gathered bf16 residual + the fresh
+    gradient, rounded to bf16), upcast to fp32 for the oracle (the reference raises on bf16)."""
     from oracle import multiworker as MW
     from oracle import powersgd_oracle as O
 
     shapes = c["shapes"]
     sizes = [numel(s) for s in shapes]
+    bf16 = c.get("dtype") == "bf16"
+    tols = PARITY_TOL_BF16 if bf16 else PARITY_TOL
     states = []
     for _ in range(world):
         st = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
@@ -348,7 +366,13 @@ def parity_check(c, world, p0, q0, outs, ress):
     res = [[torch.zeros(s) for s in shapes] for _ in range(world)]
     steps, ok, same = [], True, True
     for t in range(PARITY_STEPS):
-        grads = [[r + x for r, x in zip(res[w], parity_inputs(shapes, w, t))] for w in range(world)]
+        if bf16:
+            prev = [[torch.zeros(s) for s in shapes] if t == 0 else
+                    [x.view(s) for x, s in zip(torch.split(ress[t - 1][w], sizes), shapes)] for w in range(world)]
+            grads = [[(r + x).bfloat16().float() for r, x in zip(prev[w], parity_inputs(shapes, w, t))]
+                     for w in range(world)]
+        else:
+            grads = [[r + x for r, x in zip(res[w], parity_inputs(shapes, w, t))] for w in range(world)]
         scale = [[max(float(g.norm()), 1e-30) for g in gw] for gw in grads]
         want = MW.run_workers(states, grads)
         eo = er = 0.0
@@ -359,7 +383,7 @@ def parity_check(c, world, p0, q0, outs, ress):
                 eo = max(eo, float((got_o[i] - want[w][i].reshape(-1)).norm()) / scale[w][i])
                 er = max(er, float((got_r[i] - grads[w][i].reshape(-1)).norm()) / scale[w][i])
             same = same and torch.equal(outs[t][w], outs[t][0])
-        tol = PARITY_TOL[min(t, 1)]
+        tol = tols[min(t, 1)]
         ok = ok and eo <= tol and er <= tol  # NaN compares False
         steps.append({"max_rel_out": float(f"{eo:.3e}"), "max_rel_res": float(f"{er:.3e}"), "tol": tol})
         res = grads
@@ -381,7 +405,8 @@ def multi_gpu_parity(world, rank, dev, backend):
         try:
             for cfg in PARITY_CFGS:
                 c = CONFIGS_()[cfg]
-                psgd = PowerSGD([torch.zeros(s, device=dev) for s in c["shapes"]],
+                dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
+                psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dtype) for s in c["shapes"]],
                                 Config(c["rank"], c["mcr"], c["iters"], 0))
                 codec = psgd._powersgd
                 for buf in (codec._ps_buffer, codec._qs_buffer):  # one common injected state
@@ -390,7 +415,7 @@ def multi_gpu_parity(world, rank, dev, backend):
                     if backend != "nccl":
                         buf.copy_(host)
                 p0, q0 = codec._ps_buffer.cpu(), codec._qs_buffer.cpu()
-                outs, ress, errs = parity_collect(psgd.aggregate, c["shapes"], world, rank, backend, dev)
+                outs, ress, errs = parity_collect(psgd.aggregate, c["shapes"], world, rank, backend, dev, dtype)
                 try:
                     codec.close()
                 except RuntimeError as e:
@@ -493,7 +518,7 @@ def one_rank_group(a, dev):
     try:
         res = {"note": "world-size>1 code path on one GPU via a 1-rank RCCL process group (per-rank compute floor; "
                        "no xGMI traffic)"}
-        for cfg in ("cfg3_resnet50_r4", "cfg2_resnet50_r1"):
+        for cfg in ("cfg3_resnet50_r4", "cfg2_resnet50_r1", "cfg5_lstm_r1_i4"):
             m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
             res[cfg] = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
             res[cfg]["buckets"] = m["config"]["buckets"]

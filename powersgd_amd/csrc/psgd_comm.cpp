@@ -2,18 +2,32 @@
 // step (psgd_aggregate_comm, psgd_plan.cpp). RCCL is resolved at run time with dlopen/dlsym
 // (psgd_comm_* in include/psgd.h): an RCCL the process has already loaded (PyTorch's) is reused,
 // else PSGD_RCCL_LIB or the ROCm one; the library has no link-time dependency on it.
+// PSGD_RCCL_LIB_FORCE=<path> (tests only) takes precedence over all of these and is read at
+// every psgd_comm_unique_id / psgd_comm_init: each communicator keeps the function table of the
+// library it was created with, so one process can hold a real and a stand-in communicator
+// (tests/stubs/rccl_stub.hip drives psgd_aggregate_comm at world size W on one GPU).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "psgd.h"
 #include "psgd_internal.h"
 
+namespace psgd {
+namespace {
+struct Rccl;
+}
+}  // namespace psgd
+
 struct psgd_comm {
+    const psgd::Rccl* lib = nullptr;  // the collective library this communicator was created with
     ncclComm_t comm = nullptr;
     int world = 0, rank = -1, device = -1;
     // bucketed steps (psgd_aggregate_comm with buckets): the collectives run on this stream,
@@ -41,20 +55,24 @@ struct Rccl {
     std::string error;
 };
 
-Rccl load() {
+Rccl load(const char* forced) {
     Rccl r;
     void* h = nullptr;
-    // 1. an RCCL already in the process (the host framework's), 2. PSGD_RCCL_LIB, 3. ROCm's
-    for (const char* name : {"librccl.so", "librccl.so.1"}) {
-        if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    if (forced) {
+        h = dlopen(forced, RTLD_NOW | RTLD_LOCAL);
+    } else {
+        // 1. an RCCL already in the process (the host framework's), 2. PSGD_RCCL_LIB, 3. ROCm's
+        for (const char* name : {"librccl.so", "librccl.so.1"}) {
+            if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+        }
+        const char* env = std::getenv("PSGD_RCCL_LIB");
+        if (!h && env && *env) h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
     }
-    const char* env = std::getenv("PSGD_RCCL_LIB");
-    if (!h && env && *env) h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
     if (!h) {
         const char* de = dlerror();  // read once: a second call returns null
-        r.error = std::string("cannot load librccl.so: ") + (de ? de : "?");
+        r.error = std::string("cannot load ") + (forced ? forced : "librccl.so") + ": " + (de ? de : "?");
         return r;
     }
     auto sym = [&](const char* n) { return dlsym(h, n); };
@@ -71,19 +89,31 @@ Rccl load() {
     return r;
 }
 
+// The library for a new communicator: PSGD_RCCL_LIB_FORCE if set (tests), else the process's
+// RCCL. Tables live for the whole process (communicators point at them).
 const Rccl& rccl() {
-    static const Rccl r = load();
-    return r;
+    static std::mutex mu;
+    static std::map<std::string, std::unique_ptr<Rccl>> libs;
+    const char* forced = std::getenv("PSGD_RCCL_LIB_FORCE");
+    if (forced && !*forced) forced = nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    std::unique_ptr<Rccl>& slot = libs[forced ? std::string(forced) : std::string()];
+    if (!slot) slot.reset(new Rccl(load(forced)));
+    return *slot;
 }
 
-int rccl_fail(ncclResult_t e, const char* what) {
-    const Rccl& r = rccl();
+int rccl_fail(const Rccl& r, ncclResult_t e, const char* what) {
     return comm_fail(PSGD_ERR_DEVICE, (std::string(what) + ": " + (r.error_string ? r.error_string(e) : "?")).c_str());
 }
 
 }  // namespace
 
 int comm_world(const psgd_comm* c) { return c->world; }
+
+bool comm_poisoned(const psgd_comm* c, std::string* why) {
+    if (c->poisoned && why) *why = c->poison;
+    return c->poisoned;
+}
 
 void comm_poison(psgd_comm* c, const char* why) {
     if (c->poisoned) return;
@@ -103,7 +133,7 @@ hipStream_t comm_stream(psgd_comm* c) {
 }
 
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s) {
-    const Rccl& r = rccl();
+    const Rccl& r = *c->lib;
     if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
     if (c->poisoned) return comm_fail(PSGD_ERR_STATE, ("communicator unusable after an earlier failure: " + c->poison).c_str());
     ncclResult_t e = r.group_start();
@@ -121,7 +151,7 @@ int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, h
     if (e != ncclSuccess) {
         c->poisoned = true;
         c->poison = std::string(what) + ": " + (r.error_string ? r.error_string(e) : "?");
-        return rccl_fail(e, what);
+        return rccl_fail(r, e, what);
     }
     return PSGD_OK;
 }
@@ -144,7 +174,7 @@ int psgd_comm_unique_id(void* id_out) {
     if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
     ncclUniqueId id;
     const ncclResult_t e = r.get_unique_id(&id);
-    if (e != ncclSuccess) return rccl_fail(e, "ncclGetUniqueId");
+    if (e != ncclSuccess) return rccl_fail(r, e, "ncclGetUniqueId");
     std::memcpy(id_out, &id, sizeof(id));
     return PSGD_OK;
 }
@@ -165,8 +195,9 @@ int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, 
     if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
     if (e != ncclSuccess) {
         delete c;
-        return rccl_fail(e, "ncclCommInitRank");
+        return rccl_fail(r, e, "ncclCommInitRank");
     }
+    c->lib = &r;
     c->world = world;
     c->rank = rank;
     c->device = device;
@@ -177,7 +208,7 @@ int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, 
 int psgd_comm_destroy(psgd_comm* c) {
     if (!c) return PSGD_OK;
     if (c->cs) (void)hipStreamSynchronize(c->cs);
-    if (c->comm) (void)rccl().destroy(c->comm);
+    if (c->comm && c->lib) (void)c->lib->destroy(c->comm);
     if (c->cs) (void)hipStreamDestroy(c->cs);
     delete c;
     return PSGD_OK;

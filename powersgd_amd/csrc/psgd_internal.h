@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stdint.h>
 
 struct psgd_comm;  // include/psgd.h (psgd_comm.cpp)
@@ -16,6 +18,7 @@ int comm_world(const psgd_comm* c);
 hipStream_t comm_stream(psgd_comm* c);  // created on first use; null if creation failed
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
 void comm_poison(psgd_comm* c, const char* why);  // every later comm_allreduce fails (PSGD_ERR_STATE)
+bool comm_poisoned(const psgd_comm* c, std::string* why);  // checked before a step launches anything
 
 // Benchmark timing of the final pass (psgd_plan_set_timing): while set, the final-pass launch
 // records these events from its own dispatch packet (hipExtLaunchKernel), so the measured span
@@ -344,6 +347,10 @@ hipError_t launch_flat_pack_f64(const FlatArgs& a, hipStream_t s);
 // this rank's flag, waits (bounded) for every peer's flag and sums the W slots in rank order.
 constexpr int kMaxRanks = 64;
 constexpr int64_t kXchgHeader = 256;
+// byte offset, in the header, of the device copy of the sticky error word (XchgArgs::err_dev):
+// past the flags of every iteration (num_iters_per_step <= kMaxTerms)
+constexpr int64_t kXchgErrOff = 192;
+static_assert(kMaxTerms * 8 <= kXchgErrOff && kXchgErrOff + 4 <= kXchgHeader, "exchange header layout");
 struct XchgArgs {
     const char* const* peers;  // device array: the W exchange buffers (rank order, own included)
     uint64_t* own_flag;        // this rank's flag of this iteration (its own buffer)
@@ -357,7 +364,9 @@ struct XchgArgs {
     uint64_t epoch;            // step + 1
     uint32_t spin_limit;       // polls (~0.25 us apart) before a wait gives up
     int32_t world, rank;
-    int32_t* err;              // set to 1 when a wait timed out (psgd_ipc_status)
+    int32_t* err;              // set to 1 when a wait timed out (psgd_ipc_status; host-mapped)
+    int32_t* err_dev;          // device copy of `err` (this rank's buffer header, kXchgErrOff):
+                               // once set, later exchanges skip their waits and write NaN sums
     // rank-1 norm fold (non-last iterations): one workgroup per reduction item of this parity
     // (items, nitems, mats, even) writes the sum to dst and dst2 (the raw copy the next
     // iteration's kernels normalise on the fly) and the item's sum of squares to ss_out

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cassert>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -780,6 +781,13 @@ struct psgd_plan {
         // workgroup per CU, profiles/r04/regs_final_f32.txt) measured 0.152 vs 0.119 ms for the
         // unfused world-size > 1 step (profiles/r03/k) and is not built
         const int64_t fuse_mode = env_int("PSGD_FUSE_FINAL", 1);
+        if (fuse_mode != 0 && fuse_mode != 1) {  // 2 was the removed rank-4 K-term form
+            static bool warned = false;
+            if (!warned)
+                std::fprintf(stderr, "psgd: PSGD_FUSE_FINAL=%lld is not a mode (0 or 1); using 1\n",
+                             static_cast<long long>(fuse_mode));
+            warned = true;
+        }
         const bool use_mfma = env_int("PSGD_ODD_MFMA", 1) != 0;
         const bool use_rows = env_int("PSGD_ODD_ROWS", 1) != 0;
         int64_t podd = 0;
@@ -837,6 +845,8 @@ struct psgd_plan {
                    waves >= 2;
         };
         if (fuse_mode != 0 && small && rbucket <= 2) fin_ok = fits(iters - 1);
+        // the K-term form exists for ranks 1-2 only (dispatch_final_k<4> refuses any K-term nres)
+        assert(!fin_ok || rbucket <= 2);
         // Projection form (psgd_final.cuh): two power iterations at world size 1, ranks 2 and 4,
         // the last iteration's in-factor orthonormalised by Cholesky-QR (which leaves R').
         // Same register-panel geometry as the K-term form, so both can share the tile list.
@@ -1869,6 +1879,7 @@ int psgd_ipc_close(psgd_plan* p) {
     p->ipc_world = 0;
     p->ipc_rank = -1;
     if (p->xerr_host) __atomic_store_n(p->xerr_host, 0, __ATOMIC_RELEASE);  // a fresh exchange
+    PSGD_HIP(hipMemset(static_cast<char*>(p->ipc_buf) + kXchgErrOff, 0, sizeof(int32_t)));
     return PSGD_OK;
 }
 
@@ -2185,6 +2196,11 @@ int psgd_aggregate_comm(psgd_plan* p, void* const* grads, void* out, int64_t ste
         if (!f->bound) return fail(PSGD_ERR_STATE, "flat plan is not bound");
         if (f->dtype != PSGD_F32) return fail(PSGD_ERR_DTYPE, "psgd_aggregate_comm packs fp32 uncompressed tensors");
     }
+    // a poisoned communicator is refused before the step launches anything: the caller's
+    // gradients and the P/Q state stay as they were
+    std::string why;
+    if (comm_poisoned(comm, &why))
+        return fail(PSGD_ERR_STATE, ("communicator unusable after an earlier failure: " + why).c_str());
     DevScope scope(p->device);
     const int st = aggregate_comm_body(p, grads, out, step, has_flat ? f : nullptr, unc, flat_out, comm,
                                        static_cast<hipStream_t>(stream));
@@ -2345,6 +2361,7 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
         xa.world = world;
         xa.rank = p->ipc_rank;
         xa.err = p->xerr_dev;
+        xa.err_dev = reinterpret_cast<int32_t*>(static_cast<char*>(p->ipc_buf) + kXchgErrOff);
         PSGD_HIP(launch_xchg(xa, s));
     }
     return decompress_impl(p, grads, out, step, world, s, false);

@@ -1998,21 +1998,51 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
     // above): the flag is a plain system-scope store, no fence
     if (blockIdx.x == 0 && tid == 0)
         __hip_atomic_store(a.own_flag, a.epoch, PSGD_XCHG_FLAG_ORDER, __HIP_MEMORY_SCOPE_SYSTEM);
+    bool dead = false;
     if (tid < a.world && tid != a.rank) {  // lane w polls peer w: the W round trips overlap
         const uint64_t* f = reinterpret_cast<const uint64_t*>(a.peers[tid] + a.flag_off);
         uint32_t spins = 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
+        for (;;) {
+            // the device copy of the sticky error word, loaded beside the flag (no extra round
+            // trip): an earlier exchange of this rank gave up, so the ranks' epochs have drifted
+            // apart and this exchange is invalid whatever the flags say
+            const int32_t gone = __hip_atomic_load(a.err_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (gone) {
+                dead = true;
+                break;
+            }
+            if (fv >= a.epoch) break;
             if (++spins > a.spin_limit) {
-                // host-mapped sticky word (vector store, system scope): the results of this
-                // step are invalid and the host refuses every later exchange step
+                // host-mapped sticky word (vector store, system scope) and its device copy: the
+                // results of this step are invalid and the host refuses every later exchange step
                 __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(a.err_dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dead = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(10);
         }
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
     }
-    __syncthreads();
+    if (__syncthreads_or(dead)) {
+        // an invalid exchange returns NaN sums, never plausible stale ones: the
+        // factor (and, on the last iteration, the flat tensors) of this workgroup's share
+        const float nan = __builtin_nanf("");
+        if (a.items) {
+            const RedItem it = a.items[blockIdx.x];
+            const MatDesc d = a.mats[it.mat];
+            const int64_t e = (a.even ? d.qoff : d.poff) + it.start + tid;
+            if (tid < it.cnt) a.dst[e] = a.dst2[e] = nan;
+            return;
+        }
+        const int64_t stride = int64_t(gridDim.x) * kBlock;
+        for (int64_t i = int64_t(blockIdx.x) * kBlock + tid; i < a.n + a.nflat; i += stride) {
+            if (i < a.n) a.dst[i] = nan;
+            else a.flat_dst[i - a.n] = nan;
+        }
+        return;
+    }
     if (a.items) {  // one reduction item per workgroup (<= 256 consecutive factor elements)
         __shared__ float wsq[kWaves];
         __shared__ float xv[kRedItem];

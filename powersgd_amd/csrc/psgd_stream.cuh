@@ -66,7 +66,7 @@ __device__ __forceinline__ void keep(float& v) { asm volatile("" : "+v"(v)); }
 // System scope lowers to a vector `global_store_dword ... sc0 sc1`: write-through, the line
 // leaves (is dropped from) this XCD's L2 (MI355X_MICROARCH.md, the store-flavour row of the
 // visibility table), so the peer's read never depends on a writeback of the eight L2s at kernel
-// end. The flat region is written through with PSGD_ST_AUX (sc0 | nt | sc1) for the same reason.
+// end. The flat region is written through with kStAuxSlot (sc0 | sc1) for the same reason.
 __device__ __forceinline__ void st_slot(float* p, float v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -90,6 +90,12 @@ __device__ __forceinline__ void st_slot(float* p, float v) {
 // write-only k_lowrank_out slower (19.6 -> 23.0 us, cfg2 W > 1), and k_apply's run-time choice
 // cost a wave per SIMD of occupancy for no measured gain (profiles/r04/o).
 constexpr int kStAuxOutNt = 2;
+// The flat buffer of the uncompressed tensors is, at world size > 1 over the IPC exchange, this
+// rank's exchange slot that peers read over xGMI: its stores keep a fixed write-through policy
+// (sc0 | sc1, no nt: MI355X_MICROARCH.md, never nt on hand-off stores), independent of the
+// PSGD_ST_AUX build knob, so no A/B build can hand peers stale bytes.
+constexpr int kStAuxSlot = 17;
+static_assert((kStAuxSlot & 17) == 17, "IPC exchange slot stores (flat region) must be write-through: sc0 | sc1");
 // A kernel launch that honours g_kernel_timing (psgd_internal.h)
 template <typename... Args>
 inline void timed_launch(void (*k)(Args...), dim3 grid, dim3 block, hipStream_t s, Args... args) {
@@ -322,7 +328,7 @@ __device__ __forceinline__ void flat_pack_item(const FlatArgs& a, int item) {
         const int64_t j = it.start + int64_t(q) * NT + threadIdx.x;
         if (j < en.numel) {
             const uint32_t off = uint32_t(int64_t(q) * NT + threadIdx.x) * uint32_t(sizeof(T));
-            StIo<T>::st1(rf, off, a.world != 1 ? v[q] / w : v[q]);
+            StIo<T>::template st1<kStAuxSlot>(rf, off, a.world != 1 ? v[q] / w : v[q]);
             StIo<T>::st1(rx, off, 0.f);
         }
     }

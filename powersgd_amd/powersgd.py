@@ -349,27 +349,36 @@ class BasicPowerSGD(Aggregator):
             if err is None:
                 self._plan.ipc_close()
             raise RuntimeError(f"IPC exchange setup failed on rank(s) {bad}")
+        # the teardown barrier runs on a group of its own (CPU, gloo): at an uneven exit it can
+        # only meet other ranks' teardown barriers, never pair with a gradient collective of the
+        # default group
+        self._ipc_group = dist.new_group(backend="gloo")
         self._ipc_open = True
         _register_exit_close(self)
 
     def ipc_status(self) -> bool:
-        """True if a device-side exchange wait timed out since the last call (synchronous)."""
+        """True if a device-side exchange wait has timed out since the exchange was set up
+        (synchronous; sticky until ``close_ipc``). Steps enqueued after a timed-out wait return
+        NaN sums, and the next ``aggregate`` call raises."""
         return self._ipc_open and self._plan.ipc_status()
 
     def close_ipc(self, timeout: Optional[float] = None) -> None:
-        """Collective teardown of the IPC exchange: unmap the peers' buffers, then a barrier, so
-        that no rank frees its exchange buffer while a peer still maps it (include/psgd.h).
-        ``timeout`` (seconds) bounds the barrier (the exit hook uses it: a rank that died must not
-        hang the others at exit)."""
+        """Collective teardown of the IPC exchange: unmap the peers' buffers, then a barrier on
+        the exchange's own gloo group, so that no rank frees its exchange buffer while a peer
+        still maps it (include/psgd.h). Every rank must call it (``close()`` does), or leave it to
+        the exit hook. ``timeout`` (seconds) bounds the barrier (the exit hook uses it: a rank
+        that died must not hang the others at exit)."""
         if self._ipc_open:
             self._plan.ipc_close()
             self._ipc_open = False
+            group = getattr(self, "_ipc_group", None)
             if timeout is None:
-                torch.distributed.barrier()
+                torch.distributed.barrier(group=group)
             else:
                 import datetime
 
-                torch.distributed.barrier(async_op=True).wait(datetime.timedelta(seconds=timeout))
+                torch.distributed.barrier(group=group, async_op=True).wait(datetime.timedelta(seconds=timeout))
+            self._ipc_group = None
 
     def close(self) -> None:
         """Release the multi-GPU transports (collective: every rank calls it). The exchange
@@ -542,9 +551,10 @@ _EXIT_CLOSE: "weakref.WeakSet" = None
 
 
 def _register_exit_close(codec: "BasicPowerSGD") -> None:
-    """At interpreter exit, close every still-open IPC exchange collectively (bounded barrier),
-    so that a rank that finishes first does not free an exchange buffer a slower peer's last
-    exchange kernel may still read (the peers unmap before anyone frees)."""
+    """At interpreter exit, close every still-open IPC exchange (bounded barrier on the
+    exchange's own gloo group, never the default group), so that a rank that finishes first does
+    not free an exchange buffer a slower peer's last exchange kernel may still read (the peers
+    unmap before anyone frees). Explicit ``close()`` on every rank is the documented teardown."""
     global _EXIT_CLOSE
     if _EXIT_CLOSE is None:
         import atexit

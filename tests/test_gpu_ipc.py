@@ -85,8 +85,18 @@ def _timeout_worker(rank_id, initfile):
         psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(2, 1, 2, 0))
         psgd._powersgd._ipc_setup(0)
         if rank_id == 0:  # rank 1 never takes the step: rank 0's waits give up, no hang
-            psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
+            out = psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
+            # a second step enqueued before the first one's wait has given up is accepted by the
+            # host check; its exchanges see the device copy of the error word and skip the wait
+            try:
+                out2 = psgd.aggregate([torch.randn(s, device=dev) for s in shapes])
+            except RuntimeError as e:  # the first wait had already given up: refused
+                assert "timed out" in str(e)
+                out2 = None
             torch.cuda.synchronize()
+            # invalid sums come back as NaN, never as plausible stale values
+            for o in out + (out2 or []):
+                assert torch.isnan(o).any(), o
             assert psgd._powersgd.ipc_status()
             assert psgd._powersgd.ipc_status()  # sticky: the exchange stays invalid
             # the next step refuses to run on an invalid exchange instead of returning stale sums

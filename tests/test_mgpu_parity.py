@@ -46,23 +46,29 @@ def test_threaded_workers_match_reference_gloo_goldens(key):
     assert worst < 1e-5, worst  # W = 4: gloo sums in another order (rounding only)
 
 
-def _pipeline_worker(rank, world, initfile, corrupt, q):
+def _pipeline_worker(rank, world, initfile, corrupt, q, dtype="f32"):
     torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank, world_size=world)
     torch.set_num_threads(1)
     try:
-        c = dict(shapes=[(48, 32), (48, 32), (64, 8, 3, 3), (16,), (100, 20)], rank=2, iters=2, mcr=2)
+        c = dict(shapes=[(48, 32), (48, 32), (64, 8, 3, 3), (16,), (100, 20)], rank=2, iters=2, mcr=2,
+                 dtype=dtype)
         st = O.policy_init([torch.zeros(s) for s in c["shapes"]], c["rank"], c["mcr"], c["iters"], 0)
         for buf in (st.codec.p_flat, st.codec.q_flat):  # one common injected state
             torch.distributed.broadcast(buf, src=0)
 
         def step(grads):  # the reference restatement over the real gloo all-reduce
-            outs = O.policy_step(st, grads, world, lambda b: torch.distributed.all_reduce(b))
+            g32 = [g.float() for g in grads]  # bf16: the device path's fp32 arithmetic on bf16 storage
+            outs = O.policy_step(st, g32, world, lambda b: torch.distributed.all_reduce(b))
+            for g, r in zip(grads, g32):
+                if g is not r:
+                    g.copy_(r)  # the residual, stored in bf16
             if corrupt and rank == 1:
-                outs[2] = outs[2] + 1e-3
+                outs[2] = outs[2] + (5e-2 if dtype == "bf16" else 1e-3)  # above each dtype's bound
             return outs
 
         p0, q0 = st.codec.p_flat.clone(), st.codec.q_flat.clone()
-        outs, ress, errs = bench.parity_collect(step, c["shapes"], world, rank, "gloo", torch.device("cpu"))
+        dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        outs, ress, errs = bench.parity_collect(step, c["shapes"], world, rank, "gloo", torch.device("cpu"), dt)
         if rank == 0:
             q.put(bench.parity_check(c, world, p0, q0, outs, ress) | {"errs": errs})
     finally:
@@ -84,3 +90,22 @@ def test_gather_and_oracle_pipeline_gloo(corrupt):
     else:
         assert r["ok"] and r["outputs_equal_on_all_ranks"], r
         assert all(s["max_rel_out"] == 0.0 and s["max_rel_res"] == 0.0 for s in r["steps"]), r
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gather_and_oracle_pipeline_gloo_bf16(corrupt):
+    """bf16 gradients (cfg4's dtype): rank 0 rebuilds every worker's input from its gathered
+    bf16 residual, so the oracle sees exactly the values the step saw; the outputs match
+    bitwise, the bf16-stored residuals within bf16 rounding, and a corrupted rank is caught."""
+    ctx = torch.multiprocessing.get_context("spawn")
+    q = ctx.SimpleQueue()
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_pipeline_worker, args=(2, os.path.join(td, "init"), corrupt, q, "bf16"),
+                                    nprocs=2, join=True)
+    r = q.get()
+    assert r["errs"] == [None, None]
+    if corrupt:
+        assert not r["ok"]
+    else:
+        assert r["ok"] and r["outputs_equal_on_all_ranks"], r
+        assert all(s["max_rel_out"] == 0.0 and s["max_rel_res"] <= 4e-3 for s in r["steps"]), r
