@@ -233,9 +233,6 @@ def main():
         # the same step with every factor all-reduce as a one-shot sum over IPC exchange buffers
         # (device-side flags, no collective library): beside the RCCL headline, not instead of it
         out["ipc_exchange"] = ipc_block(a, world, rank, dev, backend)
-    if world > 1 and backend == "nccl" and "PSGD_COMM_BUCKETS" not in os.environ:
-        # the RCCL step with 2 buckets: each bucket's collective under the next bucket's kernels
-        out["rccl_buckets2"] = env_block(a, world, rank, dev, backend, {"PSGD_COMM_BUCKETS": "2"})
     if rank == 0 and world == 1:
         # the real caller's cache state: autograd's accumulation into p.grad just before
         out["post_backward"] = post_backward(a, a.config, dev)
@@ -295,7 +292,8 @@ def CONFIGS_():
 PARITY_STEPS = 2
 # every config BASELINE names for the multi-GPU runs (cfg3: rank 4; cfg4: bf16 with 11008-column
 # rows; cfg5: four power iterations, i.e. four collectives per step) and the headline cfg2
-PARITY_CFGS = ("cfg2_resnet50_r1", "cfg3_resnet50_r4", "cfg4_llama_r2_bf16", "cfg5_lstm_r1_i4")
+PARITY_CFGS = tuple(os.environ.get("PSGD_PARITY_CFGS", "cfg2_resnet50_r1,cfg3_resnet50_r4,cfg4_llama_r2_bf16,"
+                                                       "cfg5_lstm_r1_i4").split(","))
 PARITY_TOL = (1e-5, 1e-4)  # fp32: step 0 (same state), step 1 (free-running)
 PARITY_TOL_BF16 = (4e-3, 4e-3)  # bf16 gradient storage (the residual is stored in bf16)
 
@@ -345,6 +343,10 @@ def parity_collect(step, shapes, world, rank, backend, dev, dtype=torch.float32)
     return outs, ress, errs
 
 
+def _nanmax(a, b):
+    return b if (b != b or b > a) else a
+
+
 def parity_check(c, world, p0, q0, outs, ress):
     """Rank 0: the reference's W-worker steps on the same inputs from the same P/Q state; the
     largest per-tensor error relative to that rank's input tensor (SURVEY §8(c) metric). bf16
@@ -380,8 +382,9 @@ def parity_check(c, world, p0, q0, outs, ress):
             got_o = torch.split(outs[t][w], sizes)
             got_r = torch.split(ress[t][w], sizes)
             for i in range(len(shapes)):
-                eo = max(eo, float((got_o[i] - want[w][i].reshape(-1)).norm()) / scale[w][i])
-                er = max(er, float((got_r[i] - grads[w][i].reshape(-1)).norm()) / scale[w][i])
+                # NaN-propagating maximum (max() would keep the earlier value)
+                eo = _nanmax(eo, float((got_o[i] - want[w][i].reshape(-1)).norm()) / scale[w][i])
+                er = _nanmax(er, float((got_r[i] - grads[w][i].reshape(-1)).norm()) / scale[w][i])
             same = same and torch.equal(outs[t][w], outs[t][0])
         tol = tols[min(t, 1)]
         ok = ok and eo <= tol and er <= tol  # NaN compares False
@@ -396,6 +399,8 @@ def multi_gpu_parity(world, rank, dev, backend):
     from powersgd_amd import Config, PowerSGD
 
     transports = ("rccl", "ipc") if backend == "nccl" else ("torch", "ipc")
+    if os.environ.get("PSGD_PARITY_TRANSPORTS"):  # diagnostics: a subset
+        transports = tuple(t for t in transports if t in os.environ["PSGD_PARITY_TRANSPORTS"].split(","))
     report = {"steps": PARITY_STEPS, "world": world,
               "note": "every rank's outputs/residuals vs W reference workers from one injected P/Q state"}
     for tr in transports:
@@ -416,6 +421,12 @@ def multi_gpu_parity(world, rank, dev, backend):
                         buf.copy_(host)
                 p0, q0 = codec._ps_buffer.cpu(), codec._qs_buffer.cpu()
                 outs, ress, errs = parity_collect(psgd.aggregate, c["shapes"], world, rank, backend, dev, dtype)
+                # an IPC wait that gave up invalidates the sums (NaN): report it before close()
+                # clears the sticky status
+                waits = [None] * world
+                torch.distributed.all_gather_object(waits, bool(codec._ipc_open and codec.ipc_status()))
+                if any(waits):
+                    errs = errs + [f"IPC exchange wait timed out on rank(s) {[r for r, w in enumerate(waits) if w]}"]
                 try:
                     codec.close()
                 except RuntimeError as e:
@@ -522,14 +533,6 @@ def one_rank_group(a, dev):
             m = measure(a, cfg, 1, 0, dev, "nccl", "cold", dist_path=True)
             res[cfg] = {k: m[k] for k in ("value", "ms_per_step", "roofline", "step_roofline")}
             res[cfg]["buckets"] = m["config"]["buckets"]
-        # the bucketed overlap's launch cost with nothing to hide (one rank: no xGMI traffic)
-        os.environ["PSGD_COMM_BUCKETS"] = "2"
-        try:
-            m = measure(a, "cfg2_resnet50_r1", 1, 0, dev, "nccl", "cold", dist_path=True)
-            res["rccl_buckets2"] = {"cfg2_resnet50_r1": {"ms_per_step": m["ms_per_step"], "value": m["value"],
-                                                         "buckets": m["config"]["buckets"]}}
-        finally:
-            del os.environ["PSGD_COMM_BUCKETS"]
         # the IPC exchange path (psgd_aggregate_ipc) of the same configs: its flag handshake and
         # rank-order sums with W = 1 (own buffer only)
         os.environ["PSGD_COMM"] = "ipc"

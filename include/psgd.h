@@ -20,6 +20,11 @@
  *   psgd_aggregate_flat    PowerSGD.aggregate           powersgd/powersgd.py:64-74 (world size 1)
  *   psgd_aggregate_comm    PowerSGD.aggregate at world size W over RCCL (:64-74, :204-209)
  *   psgd_aggregate_ipc     the same over IPC exchange buffers with device-side flags (one node)
+ *   psgd_runs_*            DDP comm-hook plumbing: a DDP bucket's flat buffer
+ *                          <-> the per-parameter tensors, by a run table; the error-feedback add
+ *                          the reference gets from autograd's accumulation into p.grad
+ *                          (README.md:39-42, powersgd/__init__.py:24-25) and the per-bucket
+ *                          gather of the averaged gradients (paper-code/train_pytorch.py:106-131)
  *
  * Conventions
  *  - No torch types. Device buffers are plain pointers on the plan's device; `stream` is a
@@ -55,6 +60,7 @@ extern "C" {
 typedef struct psgd_plan psgd_plan;
 typedef struct psgd_flat psgd_flat;
 typedef struct psgd_comm psgd_comm;
+typedef struct psgd_runs psgd_runs;
 
 enum psgd_status {
     PSGD_OK = 0,
@@ -237,10 +243,10 @@ int psgd_reconstruct(psgd_plan* plan, void* const* grads, void* const* resid_out
  * is_distributed()): for every power iteration the codec kernels and an in-place SUM all-reduce
  * of the out-factor state buffer (:204-209; the last iteration's collective grouped with the
  * SUM all-reduce of the uncompressed tensors packed /W into flat_out, utils.py:43-47), then the
- * output pass (alpha = 1/W). flat may be null (no uncompressed tensors). With buckets set
- * (psgd_plan_set_buckets), the collectives run per bucket on a stream of the communicator,
- * ordered with events: bucket b's collective overlaps bucket b+1's kernels, and bucket b of the
- * next iteration waits only for bucket b's collective. */
+ * output pass (alpha = 1/W). flat may be null (no uncompressed tensors). The whole plan is
+ * one bucket here: a bucketed form (collectives on a second stream, event-ordered) was measured
+ * host-enqueue-bound and removed. A poisoned communicator (an earlier failure)
+ * is refused before anything is launched. */
 int psgd_comm_id_bytes(int64_t* bytes);
 int psgd_comm_unique_id(void* id_out);
 int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, psgd_comm** out);
@@ -266,6 +272,22 @@ int psgd_flat_pack(psgd_flat* flat, void* const* tensors, void* flat_out, int32_
  * two separate calls when the flat plan's dtype or device differs from the codec's. */
 int psgd_aggregate_flat(psgd_plan* plan, void* const* grads, void* out, int64_t step, psgd_flat* flat,
                         void* const* unc, void* flat_out, void* stream);
+
+/* ------------------------------------------ DDP bucket <-> parameter tensors ------ */
+/* A run table maps a DDP bucket's flat buffer onto per-parameter tensors: run k covers
+ * len[k] elements, bucket[bucket_off[k] + e] <-> tensors[tensor[k]][tensor_off[k] + e]. 64-bit
+ * offsets throughout (no limit on the model's element count). `tensors` at call time is a host
+ * array of ntensors device pointers (uploaded on the stream when it changes, like the codec's
+ * gradient tables). psgd_runs_add: tensors += bucket (the error-feedback add, in the tensors'
+ * dtype: fp32 / bf16 round to nearest even / fp64); psgd_runs_gather: bucket = tensors.
+ * Runs must not overlap in the tensors (add) or in the bucket (gather). */
+int psgd_runs_create(const int64_t* bucket_off, const int32_t* tensor, const int64_t* tensor_off,
+                     const int64_t* len, int32_t nruns, int32_t ntensors, int32_t dtype, psgd_runs** out);
+int psgd_runs_destroy(psgd_runs* runs);
+int psgd_runs_workspace_bytes(const psgd_runs* runs, int64_t* bytes);
+int psgd_runs_bind(psgd_runs* runs, int32_t device, void* workspace);
+int psgd_runs_add(psgd_runs* runs, const void* bucket, void* const* tensors, void* stream);
+int psgd_runs_gather(psgd_runs* runs, void* bucket, void* const* tensors, void* stream);
 
 #ifdef __cplusplus
 }

@@ -30,10 +30,6 @@ struct psgd_comm {
     const psgd::Rccl* lib = nullptr;  // the collective library this communicator was created with
     ncclComm_t comm = nullptr;
     int world = 0, rank = -1, device = -1;
-    // bucketed steps (psgd_aggregate_comm with buckets): the collectives run on this stream,
-    // ordered against the codec's stream with events (kernels of bucket b+1 overlap bucket b's
-    // collective)
-    hipStream_t cs = nullptr;
     // set by the first failed collective: the ranks' call sequences have diverged, so every
     // later call fails at once (PSGD_ERR_STATE) instead of enqueueing into a communicator whose
     // peers are waiting on a different collective (a hang elsewhere)
@@ -121,17 +117,6 @@ void comm_poison(psgd_comm* c, const char* why) {
     c->poison = why ? why : "?";
 }
 
-hipStream_t comm_stream(psgd_comm* c) {
-    if (!c->cs) {
-        int prev = -1;
-        (void)hipGetDevice(&prev);
-        if (c->device >= 0) (void)hipSetDevice(c->device);
-        if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess) c->cs = nullptr;
-        if (prev >= 0 && prev != c->device) (void)hipSetDevice(prev);
-    }
-    return c->cs;
-}
-
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s) {
     const Rccl& r = *c->lib;
     if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
@@ -207,9 +192,7 @@ int psgd_comm_init(int32_t world, int32_t rank, const void* id, int32_t device, 
 
 int psgd_comm_destroy(psgd_comm* c) {
     if (!c) return PSGD_OK;
-    if (c->cs) (void)hipStreamSynchronize(c->cs);
     if (c->comm && c->lib) (void)c->lib->destroy(c->comm);
-    if (c->cs) (void)hipStreamDestroy(c->cs);
     delete c;
     return PSGD_OK;
 }

@@ -15,7 +15,6 @@ namespace psgd {
 // two fp32 buffers, stream-ordered on s
 int comm_fail(int code, const char* msg);
 int comm_world(const psgd_comm* c);
-hipStream_t comm_stream(psgd_comm* c);  // created on first use; null if creation failed
 int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, hipStream_t s);
 void comm_poison(psgd_comm* c, const char* why);  // every later comm_allreduce fails (PSGD_ERR_STATE)
 bool comm_poisoned(const psgd_comm* c, std::string* why);  // checked before a step launches anything
@@ -339,6 +338,21 @@ hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, i
 hipError_t launch_orth_mgs(const OrthArgs& a, int nunits, int R, hipStream_t s);
 hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s);
 hipError_t launch_flat_pack_f64(const FlatArgs& a, hipStream_t s);
+
+// DDP bucket <-> parameter tensors (psgd_runs_*): one work item = up to kRunItem consecutive
+// elements of one run; k_runs<ADD> adds the bucket into the tensors or gathers them into it.
+constexpr int kRunItem = 16 * kBlock;
+struct RunItem {
+    int64_t boff, toff;  // element offsets in the bucket / in the tensor
+    int32_t tensor, cnt; // tensor index, elements (<= kRunItem)
+};
+struct RunsArgs {
+    const RunItem* items;
+    void* bucket;
+    void* const* tensors;
+    int32_t nitems;
+};
+hipError_t launch_runs(int dtype, bool add, const RunsArgs& a, hipStream_t s);
 
 // One-shot all-reduce over IPC-mapped exchange buffers (psgd_aggregate_ipc). Every rank's
 // exchange buffer: kXchgHeader bytes of per-iteration epoch flags (uint64, one per iteration),

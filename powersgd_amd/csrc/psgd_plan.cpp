@@ -455,7 +455,6 @@ struct psgd_plan {
     // benchmark timing of the final pass: event pairs recorded on the launch stream
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
-    std::vector<hipEvent_t> comm_ev;  // bucketed psgd_aggregate_comm: kernels-queued / collective-done
     size_t ev_used = 0;
     // one-shot IPC all-reduce (psgd_ipc_*, psgd_aggregate_ipc): this rank's exchange buffer
     // (hipMalloc'd so that it can be exported: flags header + 2 parities x iters slots), the
@@ -496,7 +495,6 @@ struct psgd_plan {
     bool qfold(int64_t step, bool agg) const { return qfold_ok && iters == 2 && proj_final(step, agg); }
 
     ~psgd_plan() {
-        for (auto& e : comm_ev) (void)hipEventDestroy(e);
         for (auto& e : ev_pool) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -906,6 +904,20 @@ struct psgd_flat {
     int device = -1;
     char* ws = nullptr;
     TableCache tab;  // device pointer tables of the tensors
+};
+
+// DDP bucket <-> parameter tensors (psgd_runs_*, include/psgd.h): the work items of one run
+// table and the device pointer tables of the tensors it addresses
+struct psgd_runs {
+    int dtype = 0;
+    int32_t ntensors = 0;
+    std::vector<RunItem> items;
+    int64_t bucket_numel = 0;  // one past the last bucket element any run touches
+    size_t o_ptrs = 0, o_items = 0, ws_bytes = 0;
+    bool bound = false;
+    int device = -1;
+    char* ws = nullptr;
+    TableCache tab;
 };
 
 namespace {
@@ -2150,6 +2162,85 @@ int psgd_flat_pack(psgd_flat* f, void* const* tensors, void* flat, int32_t world
     return PSGD_OK;
 }
 
+// ------------------------------------------------------ DDP run tables (psgd_runs) --
+int psgd_runs_create(const int64_t* bucket_off, const int32_t* tensor, const int64_t* tensor_off,
+                     const int64_t* len, int32_t nruns, int32_t ntensors, int32_t dtype, psgd_runs** out) {
+    if (!out) return fail(PSGD_ERR_VALUE, "null argument");
+    *out = nullptr;
+    if (nruns < 0 || ntensors < 0 || (nruns > 0 && (!bucket_off || !tensor || !tensor_off || !len)))
+        return fail(PSGD_ERR_VALUE, "bad run table");
+    if (dtype != PSGD_F32 && dtype != PSGD_BF16 && dtype != PSGD_F64)
+        return fail(PSGD_ERR_DTYPE, "dtype must be fp32, bf16 or fp64");
+    auto* r = new psgd_runs();
+    r->dtype = dtype;
+    r->ntensors = ntensors;
+    for (int32_t k = 0; k < nruns; ++k) {
+        if (len[k] < 0 || bucket_off[k] < 0 || tensor_off[k] < 0 || tensor[k] < 0 || tensor[k] >= ntensors) {
+            delete r;
+            return fail(PSGD_ERR_VALUE, "run " + std::to_string(k) + " out of range");
+        }
+        for (int64_t e = 0; e < len[k]; e += kRunItem)
+            r->items.push_back(RunItem{bucket_off[k] + e, tensor_off[k] + e, tensor[k],
+                                       int32_t(std::min<int64_t>(kRunItem, len[k] - e))});
+        r->bucket_numel = std::max(r->bucket_numel, bucket_off[k] + len[k]);
+    }
+    if (r->items.size() > size_t(INT32_MAX)) {
+        delete r;
+        return fail(PSGD_ERR_VALUE, "run table too large for one launch");
+    }
+    r->o_ptrs = 0;
+    r->o_items = align256(TableCache::bytes(size_t(std::max(ntensors, 1))));
+    r->ws_bytes = align256(r->o_items + std::max<size_t>(r->items.size(), 1) * sizeof(RunItem));
+    *out = r;
+    return PSGD_OK;
+}
+
+int psgd_runs_destroy(psgd_runs* r) {
+    delete r;
+    return PSGD_OK;
+}
+
+int psgd_runs_workspace_bytes(const psgd_runs* r, int64_t* bytes) {
+    if (!r || !bytes) return fail(PSGD_ERR_VALUE, "null argument");
+    *bytes = int64_t(r->ws_bytes);
+    return PSGD_OK;
+}
+
+int psgd_runs_bind(psgd_runs* r, int32_t device, void* workspace) {
+    if (!r || !workspace) return fail(PSGD_ERR_VALUE, "null argument");
+    DevScope scope(device);
+    r->device = device;
+    r->ws = static_cast<char*>(workspace);
+    r->tab.bind(r->ws + r->o_ptrs, size_t(r->ntensors));
+    if (int st = upload(r->ws + r->o_items, r->items.data(), r->items.size() * sizeof(RunItem))) return st;
+    r->bound = true;
+    return PSGD_OK;
+}
+
+static int runs_launch(psgd_runs* r, const void* bucket, void* const* tensors, bool add, void* stream) {
+    if (!r || (!bucket && !r->items.empty()) || (!tensors && r->ntensors > 0)) return fail(PSGD_ERR_VALUE, "null argument");
+    if (!r->bound) return fail(PSGD_ERR_STATE, "run table is not bound");
+    if (r->items.empty()) return PSGD_OK;
+    DevScope scope(r->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    PSGD_HIP(r->tab.select(tensors, s));
+    RunsArgs a{};
+    a.items = reinterpret_cast<const RunItem*>(r->ws + r->o_items);
+    a.bucket = const_cast<void*>(bucket);
+    a.tensors = r->tab.table();
+    a.nitems = int32_t(r->items.size());
+    PSGD_HIP(launch_runs(r->dtype, add, a, s));
+    return PSGD_OK;
+}
+
+int psgd_runs_add(psgd_runs* r, const void* bucket, void* const* tensors, void* stream) {
+    return runs_launch(r, bucket, tensors, true, stream);
+}
+
+int psgd_runs_gather(psgd_runs* r, void* bucket, void* const* tensors, void* stream) {
+    return runs_launch(r, bucket, tensors, false, stream);
+}
+
 // World-size-1 entry (psgd_aggregate / psgd_aggregate_flat): the pointer tables are selected
 // (or uploaded) on the caller's stream, then the step's launches follow on it.
 static int aggregate_entry(psgd_plan* p, void* const* grads, void* out, int64_t step, hipStream_t s,
@@ -2223,41 +2314,6 @@ static int aggregate_comm_body(psgd_plan* p, void* const* grads, void* out, int6
         if (int st = flat_args(f, unc, flat_out, world, s, &fa)) return st;
     } else if (has_flat) {
         if (int st = psgd_flat_pack(f, unc, flat_out, world, stream)) return st;
-    }
-    const int nb = int(p->spans.size());
-    hipStream_t cs = nb > 1 ? comm_stream(comm) : nullptr;
-    if (nb > 1 && cs) {
-        // buckets of shape groups (psgd_plan_set_buckets): bucket b's collective runs on the
-        // communicator's stream as soon as bucket b's kernels are queued, under bucket b+1's
-        // kernels; bucket b of the next iteration waits only for bucket b's collective
-        if (p->comm_ev.size() < size_t(2 * nb)) {
-            for (auto& e : p->comm_ev) (void)hipEventDestroy(e);
-            p->comm_ev.assign(size_t(2 * nb), nullptr);
-            for (auto& e : p->comm_ev) PSGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        hipEvent_t* ev_k = p->comm_ev.data();       // kernels of bucket b queued on s
-        hipEvent_t* ev_c = p->comm_ev.data() + nb;  // collective of bucket b done on cs
-        for (int it = 0; it < p->iters; ++it) {
-            const bool e = p->even(step, it);
-            const bool last = it == p->iters - 1;
-            for (int b = 0; b < nb; ++b) {
-                const psgd_plan::Span& sp = p->spans[size_t(b)];
-                if (it > 0) PSGD_HIP(hipStreamWaitEvent(s, ev_c[b], 0));
-                if (int st = compress_impl(p, grads, step, it, s, false, false, (fold && b == 0) ? &fa : nullptr, &sp))
-                    return st;
-                PSGD_HIP(hipEventRecord(ev_k[b], s));
-                PSGD_HIP(hipStreamWaitEvent(cs, ev_k[b], 0));
-                float* buf = e ? p->Q + sp.q[0] : p->P + sp.p[0];
-                const size_t n = size_t(e ? sp.q[1] - sp.q[0] : sp.p[1] - sp.p[0]);
-                const bool tail = last && b == nb - 1 && has_flat;
-                if (int st = comm_allreduce(comm, buf, n, tail ? static_cast<float*>(flat_out) : nullptr,
-                                            tail ? size_t(f->total) : 0, cs))
-                    return st;
-                PSGD_HIP(hipEventRecord(ev_c[b], cs));
-            }
-        }
-        for (int b = 0; b < nb; ++b) PSGD_HIP(hipStreamWaitEvent(s, ev_c[b], 0));
-        return decompress_impl(p, grads, out, step, world, s, false);
     }
     for (int it = 0; it < p->iters; ++it) {
         if (int st = compress_impl(p, grads, step, it, s, false, false, fold ? &fa : nullptr)) return st;

@@ -2153,4 +2153,71 @@ hipError_t launch_flat_pack(int dtype, const FlatArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- DDP run tables
+// The DDP comm hook's two bucket passes (powersgd_amd/ddp.py): ADD folds a bucket
+// of fresh gradients into the per-parameter error-feedback residual (what autograd's
+// accumulation into p.grad does in the reference flow, README.md:39-42: one add in the
+// gradient dtype, bf16 rounded to nearest even), GATHER copies the averaged gradients back into
+// the bucket's layout. One item per workgroup: 16 coalesced elements per thread, every load in
+// flight before any store.
+template <typename T>
+struct RunMath {  // fp32 / fp64: native adds
+    using A = T;
+    static __device__ __forceinline__ A up(T x) { return x; }
+    static __device__ __forceinline__ T down(A x) { return x; }
+};
+template <>
+struct RunMath<bf16_t> {
+    using A = float;
+    static __device__ __forceinline__ A up(bf16_t x) { return bf2f(x); }
+    static __device__ __forceinline__ bf16_t down(A x) { return f2bf(x); }
+};
+
+template <typename T, bool ADD>
+__global__ __launch_bounds__(kBlock) void k_runs(RunsArgs a) {
+    using M = RunMath<T>;
+    const RunItem it = a.items[blockIdx.x];
+    T* t = static_cast<T*>(a.tensors[it.tensor]) + it.toff;
+    T* b = static_cast<T*>(a.bucket) + it.boff;
+    constexpr int PER = kRunItem / kBlock;
+    T v[PER], w[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = q * kBlock + int(threadIdx.x);
+        const int jj = j < it.cnt ? j : 0;  // clamped, unconditional
+        if constexpr (ADD) {
+            v[q] = b[jj];
+            w[q] = t[jj];
+        } else {
+            v[q] = t[jj];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int j = q * kBlock + int(threadIdx.x);
+        if (j < it.cnt) {
+            if constexpr (ADD)
+                t[j] = M::down(M::up(w[q]) + M::up(v[q]));  // residual + fresh gradient
+            else
+                b[j] = v[q];
+        }
+    }
+}
+
+template <typename T>
+hipError_t launch_runs_t(bool add, const RunsArgs& a, hipStream_t s) {
+    if (add)
+        k_runs<T, true><<<a.nitems, kBlock, 0, s>>>(a);
+    else
+        k_runs<T, false><<<a.nitems, kBlock, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_runs(int dtype, bool add, const RunsArgs& a, hipStream_t s) {
+    if (a.nitems <= 0) return hipSuccess;
+    if (dtype == 0) return launch_runs_t<float>(add, a, s);
+    if (dtype == 2) return launch_runs_t<double>(add, a, s);
+    return launch_runs_t<bf16_t>(add, a, s);
+}
+
 }  // namespace psgd

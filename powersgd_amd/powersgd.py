@@ -401,11 +401,6 @@ class BasicPowerSGD(Aggregator):
                 obj = [_lib.comm_unique_id() if rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
                 self._comm = _lib.Comm(world, rank, obj[0], self._dev_index)
-                # PSGD_COMM_BUCKETS > 1: the library overlaps bucket b's collective (its own
-                # stream) with bucket b+1's kernels (psgd_aggregate_comm)
-                nb = int(os.environ.get("PSGD_COMM_BUCKETS", "1"))
-                if nb > 1 and self._buckets is None:
-                    self._setup_buckets(nb)
         return self._comm or None
 
     def _attach_tail(self, numel: int) -> None:

@@ -129,8 +129,8 @@ def test_fused_final_bf16():
     o_c = O.policy_step(ora, g_c)
     torch.cuda.synchronize()
     for i in range(len(shapes)):
-        assert _rel(outs[i].float(), o_c[i], x[i]) <= 1e-2
-        assert _rel(g[i].float(), g_c[i], x[i]) <= 1e-2
+        assert _rel(outs[i].float(), o_c[i], x[i]) <= 4e-3
+        assert _rel(g[i].float(), g_c[i], x[i]) <= 4e-3
 
 
 @pytest.mark.parametrize("rank,iters", [(1, 2), (2, 2), (1, 1), (16, 2)])

@@ -146,7 +146,7 @@ def _one_rank_worker(_, initfile, cfg, steps):
             for i, g in enumerate(scale):
                 tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
                 if dt == torch.bfloat16:
-                    tol = 1e-2  # bf16 gradient storage
+                    tol = 4e-3  # bf16 gradient storage; ~1.1e-3 RMS rounding
                 eo = float((od[i].cpu().double() - oc[i].double()).norm()) / max(float(g.norm()), 1e-30)
                 er = float((gd[i].cpu().double() - gc[i].double()).norm()) / max(float(g.norm()), 1e-30)
                 check(eo, tol, cfg, 0, t, i, "ipc1-out")

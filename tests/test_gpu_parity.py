@@ -11,7 +11,7 @@ Tolerances (fp32 floating point; north_star asks for a stated fp32 tolerance): p
 tensor ||ours - ref||_F <= TOL * ||input||_F with TOL_STEP = 1e-5 per step from an
 identical state (TOL_STEP_R1 = 1e-6 at rank 1) and TOL_FREE = 1e-4 for up to 4
 free-running steps; bf16 gradients (reference cannot run them) compare against the oracle
-on bf16-rounded inputs with TOL_BF16 = 1e-2. Every comparison's error is logged
+on bf16-rounded inputs with TOL_BF16 = 4e-3. Every comparison's error is logged
 (tests/parity_log.py); DESIGN.md §5 quotes the worst observed values.
 """
 import os
@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 TOL_STEP = 1e-5
 TOL_STEP_R1 = 1e-6  # rank 1: same op order as the reference up to summation order
 TOL_FREE = 1e-4
-TOL_BF16 = 1e-2
+TOL_BF16 = 4e-3
 DEV = torch.device("cuda:0")
 MAN = manifest()
 

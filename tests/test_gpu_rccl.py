@@ -19,8 +19,7 @@ def _rel(a, b, scale):
     return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
 
 
-def _worker(_, port, cfg, steps, buckets=1, env=None):
-    os.environ["PSGD_COMM_BUCKETS"] = str(buckets)
+def _worker(_, port, cfg, steps, env=None):
     os.environ.update(env or {})  # plan knobs, read at plan creation
     from oracle import powersgd_oracle as O
     from powersgd_amd import Config, PowerSGD, _lib
@@ -51,12 +50,10 @@ def _worker(_, port, cfg, steps, buckets=1, env=None):
             oc = O.policy_step(ora, gc)
             torch.cuda.synchronize()
             assert isinstance(psgd._powersgd._comm, _lib.Comm)  # the library's RCCL path ran
-            if buckets > 1:  # the bucketed overlap (collectives on the communicator's stream)
-                assert psgd._powersgd._buckets is not None and len(psgd._powersgd._buckets) > 1
             for i, g in enumerate(scale):
                 tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
                 if dt == torch.bfloat16:
-                    tol = 1e-2  # bf16 gradient storage
+                    tol = 4e-3  # bf16 gradient storage; ~1.1e-3 RMS rounding
                 check(_rel(od[i], oc[i], g), tol, cfg, t, i, "out")
                 check(_rel(gd[i], gc[i], g), tol, cfg, t, i, "res")
             res_d, res_c = gd, gc
@@ -72,16 +69,6 @@ def test_rccl_step_one_rank_vs_oracle(cfg):
     torch.multiprocessing.spawn(_worker, args=(port, cfg, 3), nprocs=1, join=True)
 
 
-@pytest.mark.parametrize("cfg", ["cfg3_resnet50_r4", "cfg2_resnet50_r1"])
-def test_rccl_bucketed_overlap_vs_oracle(cfg):
-    """PSGD_COMM_BUCKETS=4: per-bucket kernels on the codec's stream, per-bucket collectives on
-    the communicator's stream, ordered by events: same results as the single collective."""
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    torch.multiprocessing.spawn(_worker, args=(port, cfg, 3, 4), nprocs=1, join=True)
-
-
 def test_rccl_kterm_own_row_blocks_vs_oracle():
     """The K-term final pass on its own row blocks (psgd_plan.cpp tiles_fin_kt, MatDesc::
     fin_rows_kt) at an odd block size, 5000 elements: ragged against every ResNet-50 row length,
@@ -89,5 +76,5 @@ def test_rccl_kterm_own_row_blocks_vs_oracle():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    torch.multiprocessing.spawn(_worker, args=(port, "cfg2_resnet50_r1", 2, 1, {"PSGD_FIN_ELEMS_KT": "5000"}),
+    torch.multiprocessing.spawn(_worker, args=(port, "cfg2_resnet50_r1", 2, {"PSGD_FIN_ELEMS_KT": "5000"}),
                                 nprocs=1, join=True)

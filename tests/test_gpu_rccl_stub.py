@@ -34,7 +34,7 @@ def _rel(a, b, scale):
     return float((a.double().cpu() - b.double().cpu()).norm()) / max(float(scale.double().norm()), 1e-30)
 
 
-def _run(cfg, world, buckets, steps, port, env):
+def _run(cfg, world, steps, port, env):
     """`steps` steps of cfg at world size `world` through the stub; returns per step the largest
     output / residual errors against W oracle workers and the stub's collective count."""
     os.environ["PSGD_RCCL_LIB_FORCE"] = STUB
@@ -59,9 +59,6 @@ def _run(cfg, world, buckets, steps, port, env):
         # the library's own communicator, created through the stand-in at world W (the process
         # group itself has one rank: it only makes is_distributed() true)
         codec._comm = _lib.Comm(world, 0, _lib.comm_unique_id(), 0)
-        if buckets > 1:
-            codec._setup_buckets(buckets)
-            assert len(codec._buckets) == buckets
         states = []
         for _ in range(world):
             st = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
@@ -94,27 +91,26 @@ def _run(cfg, world, buckets, steps, port, env):
 
 
 def _positive(_, port, cfg, world, steps):
-    for buckets in (1, 2):
-        rep = _run(cfg, world, buckets, steps, _port() if buckets > 1 else port, {"PSGD_STUB_MODE": "sum"})
-        c_iters = {"cfg2_resnet50_r1": 2, "cfg3_resnet50_r4": 2, "cfg4_llama_r2_bf16": 1, "cfg5_lstm_r1_i4": 4}[cfg]
-        for t, (eo, er, calls, nunc) in enumerate(rep):
-            bf16 = cfg.startswith("cfg4")
-            tol = 4e-3 if bf16 else ((1e-5 if t == 0 else 1e-4))
-            check(eo, tol, cfg, world, buckets, t, "out")
-            check(er, tol, cfg, world, buckets, t, "res")
-            # one collective per power iteration and bucket, plus the flat tail in the last one
-            assert calls == c_iters * buckets + (1 if nunc else 0), (cfg, buckets, calls)
+    rep = _run(cfg, world, steps, port, {"PSGD_STUB_MODE": "sum"})
+    c_iters = {"cfg2_resnet50_r1": 2, "cfg3_resnet50_r4": 2, "cfg4_llama_r2_bf16": 1, "cfg5_lstm_r1_i4": 4}[cfg]
+    for t, (eo, er, calls, nunc) in enumerate(rep):
+        bf16 = cfg.startswith("cfg4")
+        tol = 4e-3 if bf16 else ((1e-5 if t == 0 else 1e-4))
+        check(eo, tol, cfg, world, t, "out")
+        check(er, tol, cfg, world, t, "res")
+        # one collective per power iteration, plus the flat tail grouped with the last one
+        assert calls == c_iters + (1 if nunc else 0), (cfg, calls)
 
 
 @pytest.mark.parametrize("cfg,world", [("cfg2_resnet50_r1", 4), ("cfg3_resnet50_r4", 4),
                                        ("cfg5_lstm_r1_i4", 8), ("cfg4_llama_r2_bf16", 2)])
 def test_rccl_orchestration_world_w_vs_oracle(cfg, world):
-    """psgd_aggregate_comm at world W (1 and 2 buckets), 2 steps each, vs W reference workers."""
+    """psgd_aggregate_comm at world W, 2 steps, vs W reference workers."""
     torch.multiprocessing.spawn(_positive, args=(_port(), cfg, world, 2), nprocs=1, join=True)
 
 
 def _negative(_, port, env, q):
-    rep = _run("cfg2_resnet50_r1", 4, 1, 1, port, env)
+    rep = _run("cfg2_resnet50_r1", 4, 1, port, env)
     q.put(max(rep[0][0], rep[0][1]))
 
 

@@ -1,7 +1,8 @@
 """A few plain cfg2 steps through the library's RCCL path on a 1-rank RCCL group (the W > 1 code
 path on one GPU), for a kernel + HIP API trace of the bucketed overlap (PSGD_COMM_BUCKETS=2)
 against the single-collective step. Run under rocprofv3; prints the mean ms per step.
-usage: PSGD_COMM_BUCKETS=2 rocprofv3 --kernel-trace --hip-runtime-trace ... -- python3 tools/bucket_trace.py [steps]"""
+usage: rocprofv3 --kernel-trace --hip-runtime-trace ... -- python3 tools/bucket_trace.py [steps]
+(round 5 traced PSGD_COMM_BUCKETS=2 with it, profiles/r05/bucket_trace; that mode is removed since)"""
 import os
 import socket
 import sys

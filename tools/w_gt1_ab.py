@@ -1,6 +1,6 @@
 """Times the world-size > 1 code path (1-rank RCCL group, bench.one_rank_group) for cfg3 and
 cfg2 under the current environment; prints one JSON line. For A/B runs of plan knobs:
-PSGD_COMM_BUCKETS=2 python tools/w_gt1_ab.py"""
+PSGD_FIN_ELEMS_KT=12000 python tools/w_gt1_ab.py"""
 import argparse
 import json
 import os
