@@ -64,6 +64,12 @@ _SIGNATURES = {
     "psgd_aggregate_ipc": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _i32),
     "psgd_ipc_status": ([_vp, _P_i32], _i32),
     "psgd_ipc_close": ([_vp], _i32),
+    "psgd_runs_create": ([_P_i64, _P_i32, _P_i64, _P_i64, _i32, _i32, _i32, ctypes.POINTER(_vp)], _i32),
+    "psgd_runs_destroy": ([_vp], _i32),
+    "psgd_runs_workspace_bytes": ([_vp, _P_i64], _i32),
+    "psgd_runs_bind": ([_vp, _i32, _vp], _i32),
+    "psgd_runs_add": ([_vp, _vp, _vp, _vp], _i32),
+    "psgd_runs_gather": ([_vp, _vp, _vp, _vp], _i32),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -301,6 +307,40 @@ class FlatPlan:
 
     def pack(self, tensors, flat_ptr: int, world: int, stream: int) -> None:
         check(lib().psgd_flat_pack(self._h, tensors, flat_ptr, world, stream))
+
+
+class Runs:
+    """Owns a psgd_runs: a DDP bucket's flat buffer <-> per-parameter tensors (run table, 64-bit
+    offsets). ``add``: tensors += bucket (error-feedback add); ``gather``: bucket = tensors."""
+
+    def __init__(self, bucket_off: Sequence[int], tensor: Sequence[int], tensor_off: Sequence[int],
+                 length: Sequence[int], ntensors: int, dtype_code: int):
+        n = len(length)
+        h = _vp()
+        check(lib().psgd_runs_create((_i64 * max(1, n))(*bucket_off), (_i32 * max(1, n))(*tensor),
+                                     (_i64 * max(1, n))(*tensor_off), (_i64 * max(1, n))(*length), n, ntensors,
+                                     dtype_code, ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.psgd_runs_destroy(h)
+            self._h = None
+
+    def workspace_bytes(self) -> int:
+        b = _i64()
+        check(lib().psgd_runs_workspace_bytes(self._h, ctypes.byref(b)))
+        return b.value
+
+    def bind(self, device: int, ws_ptr: int) -> None:
+        check(lib().psgd_runs_bind(self._h, device, ws_ptr))
+
+    def add(self, bucket_ptr: int, tensors, stream: int) -> None:
+        check(lib().psgd_runs_add(self._h, bucket_ptr, tensors, stream))
+
+    def gather(self, bucket_ptr: int, tensors, stream: int) -> None:
+        check(lib().psgd_runs_gather(self._h, bucket_ptr, tensors, stream))
 
 
 def comm_unique_id() -> bytes:

@@ -20,6 +20,11 @@ how DDP buckets the parameters (and of its bucket rebuild after the first iterat
   layout. DDP waits on all bucket futures only after backward has launched every hook, so the
   deferral is legal; it trades DDP's per-bucket overlap for the reference's exact semantics.
 
+Bucket plumbing is native (include/psgd.h ``psgd_runs_*``): per DDP bucket layout a run table
+(bucket offset, parameter, length: one run per parameter, 64-bit offsets) drives one HIP launch
+that adds the bucket into the residual and, at completion, one that gathers the averages back
+into the bucket buffer. No index maps, no full-size copy, no limit on the element count.
+
 Because the residual lives in the state (not in ``p.grad``), the training loop zeroes
 gradients as usual:
 
@@ -28,12 +33,29 @@ gradients as usual:
     ddp_model.register_comm_hook(state, powersgd_hook)
     loss.backward(); optimizer.step(); optimizer.zero_grad()
 """
+import ctypes
 from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
-from .powersgd import Config, PowerSGD
+from . import _lib
+from .powersgd import Config, PowerSGD, _DTYPES, _psgd_host, _require_device, _stream
+
+
+class _BucketRuns:
+    """The run table of one DDP bucket layout (one run per parameter: bucket offset, parameter
+    index, length), bound to device memory (psgd_runs_*)."""
+
+    def __init__(self, key, buf: torch.Tensor, grads, idx, ntensors: int, code: int, dev_index: int):
+        self.key = key
+        esz = buf.element_size()
+        self.offs = [(g.data_ptr() - buf.data_ptr()) // esz for g in grads]
+        self.idx = list(idx)
+        self.lens = [g.numel() for g in grads]
+        self.runs = _lib.Runs(self.offs, self.idx, [0] * len(idx), self.lens, ntensors, code)
+        self.ws = torch.empty(self.runs.workspace_bytes(), dtype=torch.uint8, device=buf.device)
+        self.runs.bind(dev_index, self.ws.data_ptr())
 
 
 class PowerSGDState:
@@ -49,17 +71,23 @@ class PowerSGDState:
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         numel = sum(p.numel() for p in self.params)
         p0 = self.params[0]
+        self._dev_index = _require_device(p0.device)
+        self._code = _DTYPES[p0.dtype] if p0.dtype in _DTYPES else None
+        if self._code is None:
+            raise RuntimeError(f"powersgd_hook supports float32, bfloat16 and float64 gradients, got {p0.dtype}")
         self.residual = torch.zeros(numel, dtype=p0.dtype, device=p0.device)
         self.views: List[torch.Tensor] = []
-        self._offs: List[int] = []
         off = 0
         for p in self.params:
-            self._offs.append(off)
             self.views.append(self.residual[off:off + p.numel()].view(p.shape))
             off += p.numel()
-        # per DDP bucket index: (layout key, int32 device index map) of its LATEST layout only
-        # (DDP rebuilds its buckets after the first iteration; the old maps are dropped)
-        self._gidx: Dict[int, tuple] = {}
+        # per-parameter pointer tables (host arrays handed to psgd_runs_*): the residual views
+        # (fixed) and the latest averaged outputs (refilled natively at every completion)
+        self._res_ptrs = _lib.ptr_array([v.data_ptr() for v in self.views])
+        self._out_ptrs = _lib.ptr_array([0] * len(self.views))
+        # per DDP bucket index: the run table of its LATEST layout only (DDP rebuilds its buckets
+        # after the first iteration; the old tables are dropped)
+        self._runs: Dict[int, _BucketRuns] = {}
         self.powersgd = PowerSGD(self.views, config)
         self._seen = [False] * len(self.params)
         self._nseen = 0
@@ -78,14 +106,12 @@ class PowerSGDState:
                     raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
                 idx.append(i)
             buf = bucket.buffer()
-            gidx = self._gather_index(bucket.index(), buf, grads, idx)
-            # error feedback: residual + fresh gradient, the whole bucket in one indexed add
-            # (bucket buffer position -> residual position; every position once)
-            self.residual.index_add_(0, gidx, buf)
+            runs = self._bucket_runs(bucket.index(), buf, grads, idx)
+            self._ef_add(buf, runs)
             for i in idx:
                 self._seen[i] = True
                 self._nseen += 1
-            self._pending.append((buf, gidx, fut))
+            self._pending.append((buf, runs, fut))
             if self._nseen == len(self.params):
                 self._complete()
             elif bucket.is_last():
@@ -112,36 +138,44 @@ class PowerSGDState:
         if not fut.done():
             fut.set_exception(err)
 
-    def _gather_index(self, bucket_index: int, buf: torch.Tensor, grads, idx) -> torch.Tensor:
-        """Device index: position k of the bucket's flat buffer -> its position in the state's
-        flat residual. int32 (4 bytes per gradient element: index_add_ / index_select take it),
+    def _bucket_runs(self, bucket_index: int, buf: torch.Tensor, grads, idx) -> _BucketRuns:
+        """The bucket's run table (one run per parameter: bucket offset -> parameter, length),
         built once per bucket layout; only the bucket's latest layout is kept."""
         key = (buf.numel(), tuple(idx), tuple((g.data_ptr() - buf.data_ptr()) // buf.element_size() for g in grads))
-        hit = self._gidx.get(bucket_index)
-        if hit is not None and hit[0] == key:
-            return hit[1]
-        if self.residual.numel() >= 2 ** 31:
-            raise RuntimeError("powersgd_hook: more than 2^31 gradient elements (int32 index maps)")
-        host = torch.empty(buf.numel(), dtype=torch.int32)
-        for g, i in zip(grads, idx):
-            off = (g.data_ptr() - buf.data_ptr()) // buf.element_size()
-            host[off:off + g.numel()] = torch.arange(self._offs[i], self._offs[i] + g.numel(), dtype=torch.int32)
-        self._gidx.pop(bucket_index, None)  # free the stale layout's map before the new upload
-        gidx = host.to(buf.device)
-        self._gidx[bucket_index] = (key, gidx)
-        return gidx
+        hit = self._runs.get(bucket_index)
+        if hit is not None and hit.key == key:
+            return hit
+        self._runs.pop(bucket_index, None)
+        r = self._new_runs(key, buf, grads, idx)
+        self._runs[bucket_index] = r
+        return r
+
+    def _new_runs(self, key, buf, grads, idx) -> _BucketRuns:
+        return _BucketRuns(key, buf, grads, idx, len(self.params), self._code, self._dev_index)
+
+    def _ef_add(self, buf: torch.Tensor, runs: _BucketRuns) -> None:
+        """Error feedback: residual += the bucket's fresh gradients, the whole bucket in one launch
+        (autograd's accumulation into p.grad in the reference flow, README.md:39-42)."""
+        runs.runs.add(buf.data_ptr(), ctypes.addressof(self._res_ptrs), _stream(buf.device))
+
+    def _gather(self, pending, outs) -> None:
+        """The averages, parameter by parameter, straight into each pending bucket's buffer (its
+        own layout), one launch per bucket on the codec's stream."""
+        _psgd_host.fill_list(outs, ctypes.addressof(self._out_ptrs), self._code, self._dev_index)
+        stream = _stream(self.residual.device)
+        for buf, runs, _ in pending:
+            runs.runs.gather(buf.data_ptr(), ctypes.addressof(self._out_ptrs), stream)
 
     def _complete(self) -> None:
         outs = self.powersgd.aggregate(self.views)  # leaves the new residual in self.views
         pending, self._pending = self._pending, []
         self._seen = [False] * len(self.params)
         self._nseen = 0
-        # the averages in the state's order (a transient copy: the compressed and uncompressed
-        # outputs live in two buffers), then one gather per bucket, in its layout
-        flat = torch.cat([o.reshape(-1) for o in outs])
-        for buf, gidx, fut in pending:
-            fut.set_result(flat.index_select(0, gidx))
-        del flat
+        # the gathers read `outs` on the stream; the codec reuses its output buffer only at a later
+        # aggregate (same stream) once no view of it is referenced: queued before that, safe
+        self._gather(pending, outs)
+        for buf, _, fut in pending:
+            fut.set_result(buf)
 
 
 def powersgd_hook(state: PowerSGDState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:

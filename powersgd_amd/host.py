@@ -24,6 +24,14 @@ the codec on the GPUs:
   scattered to the bins, so results equal the single-process reference (tests/test_gpu_host.py).
 * Uncompressed tensors never leave the host: at world size 1 ``AllReduce`` is a copy plus a
   zero (:22-31, utils.py:43-49).
+* ``residual="device"`` (opt-in semantic variant): the error-feedback residual of the
+  compressed tensors stays on the GPU between steps and only the outputs return over PCIe
+  (half the outbound bytes). Each ``aggregate`` then takes the FRESH gradients (the caller
+  zeroes ``p.grad`` every step, e.g. ``optimizer.zero_grad()``, as with the DDP hook) and adds
+  them to the device residual on the GPU — the same single add autograd's accumulation into
+  ``p.grad`` performs in the reference flow (README.md:39-42), so the numbers are identical; the
+  compressed inputs are left untouched instead of being overwritten with the residual.
+  ``residual()`` copies the device residual back on demand.
 """
 from __future__ import annotations
 
@@ -40,8 +48,11 @@ class HostPowerSGD:
     """Drop-in for ``powersgd.PowerSGD`` on CPU parameters (world size 1)."""
 
     def __init__(self, params: List[torch.Tensor], config: Config, devices: Optional[Sequence[int]] = None,
-                 chunks: int = 2):
+                 chunks: int = 2, residual: str = "host"):
         params = list(params)
+        if residual not in ("host", "device"):
+            raise ValueError("residual must be 'host' (the reference's contract) or 'device'")
+        self.residual_on_device = residual == "device"
         if is_distributed():
             # world-size-1 semantics only: the factors of every bin would be all-reduced while
             # the uncompressed and warm-up paths stay local (a mix of global and local means)
@@ -117,6 +128,8 @@ class HostPowerSGD:
                     self.streams[bn["dev"]] = (torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev))
             with torch.cuda.device(dev):
                 bn["dflat"] = torch.zeros(bn["hi"] - bn["lo"], dtype=self.dtype, device=dev)
+                if self.residual_on_device:  # the fresh gradients land here, then add into dflat
+                    bn["dstage"] = torch.zeros(bn["hi"] - bn["lo"], dtype=self.dtype, device=dev)
                 bn["dgrads"] = [self._view(bn["dflat"], i, base=bn["lo"]) for i in bn["idx"]]
                 codec = BasicPowerSGD(bn["dgrads"], BasicConfig(config.rank, config.num_iters_per_step))
                 codec._ps_buffer.copy_(torch.cat([p0[k].reshape(-1) for k in bn["keys"]]))
@@ -176,15 +189,19 @@ class HostPowerSGD:
             self._out_views[i].copy_(gradients[i])
             gradients[i].zero_()
         # pipeline: H2D (stream 0) -> codec (stream 1) -> D2H (stream 2), per device
+        dres = self.residual_on_device
         for bn in self.bins:
             s_in, _, _ = self.streams[bn["dev"]]
             with torch.cuda.device(bn["dev"]), torch.cuda.stream(s_in):
-                bn["dflat"].copy_(self.host_grads[bn["lo"]:bn["hi"]], non_blocking=True)
+                dst = bn["dstage"] if dres else bn["dflat"]
+                dst.copy_(self.host_grads[bn["lo"]:bn["hi"]], non_blocking=True)
                 bn["events"][0].record(s_in)
         for bn in self.bins:
             _, s_comp, _ = self.streams[bn["dev"]]
             with torch.cuda.device(bn["dev"]), torch.cuda.stream(s_comp):
                 s_comp.wait_event(bn["events"][0])
+                if dres:  # residual + fresh gradient (autograd's accumulation, on the device)
+                    bn["dflat"].add_(bn["dstage"])
                 bn["codec"].aggregate(bn["dgrads"])
                 bn["events"][1].record(s_comp)
         for bn in self.bins:
@@ -193,11 +210,22 @@ class HostPowerSGD:
                 s_out.wait_event(bn["events"][1])
                 slab = bn["codec"]._slab.flat[:bn["hi"] - bn["lo"]]
                 self.host_out[bn["lo"]:bn["hi"]].copy_(slab, non_blocking=True)
-                self.host_grads[bn["lo"]:bn["hi"]].copy_(bn["dflat"], non_blocking=True)
+                if not dres:
+                    self.host_grads[bn["lo"]:bn["hi"]].copy_(bn["dflat"], non_blocking=True)
         for dev, (_, _, s_out) in self.streams.items():
             s_out.synchronize()
-        if not direct:
+        if not direct and not dres:
             for i, g in enumerate(gradients):
                 if self.is_compressed_mask[i]:
                     g.copy_(self._view(self.host_grads, i))
         return list(self._out_views)
+
+    def residual(self) -> List[torch.Tensor]:
+        """The compressed tensors' error-feedback residual (CPU copies; ``residual="device"``:
+        from the GPU, synchronously). Uncompressed tensors have none (zero)."""
+        out = [torch.zeros(s, dtype=self.dtype) for s in self.shapes]
+        for bn in self.bins:
+            host = bn["dflat"].cpu() if self.residual_on_device else self.host_grads[bn["lo"]:bn["hi"]]
+            for i in bn["idx"]:
+                out[i].copy_(self._view(host, i, base=bn["lo"]))
+        return out

@@ -50,21 +50,43 @@ class _Codec:
         return [v.clone() for v in views]
 
 
+class _CpuRuns:
+    """The run table the hook builds per bucket layout (bucket offset, parameter, length), with
+    the two native passes (psgd_runs_add / psgd_runs_gather) emulated on CPU tensors."""
+
+    def __init__(self, key, buf, grads, idx):
+        self.key = key
+        self.offs = [(g.data_ptr() - buf.data_ptr()) // buf.element_size() for g in grads]
+        self.idx = list(idx)
+        self.lens = [g.numel() for g in grads]
+
+
 def _state(params, codec):
     st = object.__new__(PowerSGDState)  # the constructor builds a GPU codec: bypass it
     st.params = params
     st._index = {id(p): i for i, p in enumerate(params)}
     st.residual = torch.zeros(sum(p.numel() for p in params))
-    st.views, st._offs, off = [], [], 0
+    st.views, off = [], 0
     for p in params:
-        st._offs.append(off)
         st.views.append(st.residual[off:off + p.numel()].view(p.shape))
         off += p.numel()
-    st._gidx = {}
+    st._runs = {}
     st.powersgd = codec
     st._seen = [False] * len(params)
     st._nseen = 0
     st._pending = []
+    st._new_runs = lambda key, buf, grads, idx: _CpuRuns(key, buf, grads, idx)
+
+    def ef_add(buf, runs):
+        for o, i, n in zip(runs.offs, runs.idx, runs.lens):
+            st.views[i].view(-1).add_(buf[o:o + n])
+
+    def gather(pending, outs):
+        for buf, runs, _ in pending:
+            for o, i, n in zip(runs.offs, runs.idx, runs.lens):
+                buf[o:o + n].copy_(outs[i].reshape(-1))
+
+    st._ef_add, st._gather = ef_add, gather
     return st
 
 
@@ -123,18 +145,20 @@ def test_unknown_parameter_and_double_arrival():
     assert st._nseen == 0
 
 
-def test_index_maps_are_int32_and_only_the_latest_layout_is_kept():
-    """A DDP bucket rebuild (new layout under the same bucket index) replaces that bucket's
-    index map; maps are int32 (4 bytes per gradient element)."""
+def test_run_tables_one_run_per_parameter_and_only_the_latest_layout_is_kept():
+    """A DDP bucket rebuild (new layout under the same bucket index) replaces that bucket's run
+    table; a table holds one (bucket offset, parameter, length) run per parameter, nothing per
+    element (no index maps: the hook scales past 2^31 gradient elements)."""
     ps = _params()
     st = _state(ps, _Codec())
     powersgd_hook(st, _Bucket(ps[:2], False, index=0))
     powersgd_hook(st, _Bucket(ps[2:], True, index=1))
-    assert sorted(st._gidx) == [0, 1] and all(v[1].dtype == torch.int32 for v in st._gidx.values())
+    assert sorted(st._runs) == [0, 1]
+    assert st._runs[0].offs == [0, 8] and st._runs[0].idx == [0, 1] and st._runs[0].lens == [8, 8]
     # rebuilt buckets: parameter 2 moves into bucket 0
     f0 = powersgd_hook(st, _Bucket([ps[2], ps[0]], False, index=0))
     f1 = powersgd_hook(st, _Bucket(ps[1:2], True, index=1))
-    assert sorted(st._gidx) == [0, 1]
-    assert st._gidx[0][1].numel() == 16 and st._gidx[1][1].numel() == 8
+    assert sorted(st._runs) == [0, 1]
+    assert st._runs[0].idx == [2, 0] and st._runs[0].offs == [0, 8] and st._runs[1].idx == [1]
     # the stub codec leaves the residual in place: two iterations of ones accumulated
     assert torch.equal(f0.value(), torch.full((16,), 2.)) and torch.equal(f1.value(), torch.full((8,), 2.))

@@ -61,3 +61,37 @@ def test_held_outputs_are_not_overwritten():
     host.aggregate([x.clone() * 3 for x in g])
     for a, b in zip(first, keep):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("pin", [False, True])
+def test_device_residual_variant_equals_reference_contract(pin):
+    """residual="device" (outputs-only D2H; the caller hands FRESH gradients each step and the
+    residual stays on the GPU) returns bitwise the outputs of the reference contract (residual
+    back in the caller's tensors, next gradient accumulated onto it), and the same residual."""
+    cfg = Config(2, 2, 2, 1)
+    p_ref = [torch.zeros(s) for s in SHAPES]
+    p_dev = [torch.zeros(s) for s in SHAPES]
+    ref = HostPowerSGD(p_ref, cfg, devices=[0, 0], chunks=2)
+    dev = HostPowerSGD(p_dev, cfg, devices=[0, 0], chunks=2, residual="device")
+    if pin:
+        dev.pin_gradients(p_dev)
+    res = [torch.zeros(s) for s in SHAPES]
+    for t in range(4):
+        fresh = [torch.from_numpy(f) for f in hash_tensors(SHAPES, seed=300 + t)]
+        g_ref = [r + f for r, f in zip(res, fresh)]
+        if pin:
+            for p, f in zip(p_dev, fresh):
+                p.grad.zero_()
+                p.grad.add_(f)  # zero_grad + backward
+            g_dev = [p.grad for p in p_dev]
+        else:
+            g_dev = [f.clone() for f in fresh]
+        out_ref = ref.aggregate(g_ref)
+        out_dev = dev.aggregate(g_dev)
+        for i in range(len(SHAPES)):
+            assert torch.equal(out_ref[i], out_dev[i]), (t, i)
+        r_dev = dev.residual()
+        for i, c in enumerate(ref.is_compressed_mask):
+            if c:
+                assert torch.equal(r_dev[i], g_ref[i]), (t, i)
+        res = [g if c else torch.zeros_like(g) for g, c in zip(g_ref, ref.is_compressed_mask)]
