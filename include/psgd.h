@@ -198,6 +198,9 @@ int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step,
  * (output G X X^T, exact for I = 2 at world size 1): *fused = 2 for that
  * form (k_final_proj; ranks 1/2/4), 1 for the K-term form (k_final_odd), 0 unfused. */
 int psgd_plan_fused_final(const psgd_plan* plan, int64_t step, int32_t aggregate, int32_t* fused);
+/* Nonzero when iteration `it` of `step` (odd, followed by an even one) runs as ONE gradient pass
+ * with the next iteration's product inside psgd_aggregate (rank 1, world size 1, I >= 3). */
+int psgd_plan_odd_even(const psgd_plan* plan, int64_t step, int32_t it, int32_t* on);
 
 /* Kernel timing for benchmarks: when enabled, every final pass launched by psgd_aggregate
  * (k_apply, or the fused final odd kernel) and by psgd_decompress (k_apply) is bracketed by HIP events recorded on its own stream.

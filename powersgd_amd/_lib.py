@@ -38,6 +38,7 @@ _SIGNATURES = {
     "psgd_decompress": ([_vp, _vp, _vp, _i64, _i32, _vp], _i32),
     "psgd_aggregate": ([_vp, _vp, _vp, _i64, _vp], _i32),
     "psgd_plan_fused_final": ([_vp, _i64, _i32, _P_i32], _i32),
+    "psgd_plan_odd_even": ([_vp, _i64, _i32, _P_i32], _i32),
     "psgd_plan_set_timing": ([_vp, _i32], _i32),
     "psgd_plan_timing_read": ([_vp, _P_dbl, _P_i32], _i32),
     "psgd_flat_create": ([_P_i64, _i32, _i32, ctypes.POINTER(_vp)], _i32),
@@ -256,6 +257,13 @@ class Plan:
         f = _i32()
         check(lib().psgd_plan_fused_final(self._h, step, 1 if aggregate else 0, ctypes.byref(f)))
         return int(f.value)
+
+    def odd_even(self, step: int, it: int) -> bool:
+        """True when odd iteration ``it`` of ``step`` runs fused with the next (even) iteration's
+        product in one gradient pass (psgd_aggregate: rank 1, world size 1, I >= 3)."""
+        f = _i32()
+        check(lib().psgd_plan_odd_even(self._h, step, it, ctypes.byref(f)))
+        return bool(f.value)
 
     # --- building blocks (paper-code reducer variants, powersgd_amd/reducers.py)
     def product(self, grads, odd: bool, x_ptr: int, y_ptr: int, terms=(), stream: int = 0) -> None:

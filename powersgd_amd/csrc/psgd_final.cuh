@@ -81,9 +81,15 @@ constexpr int kProjRows = kFinRowsMax;
 // reference's output P_0 Q_0^T + P_1 X^T is exactly s X^T per row, s = G X + (N - c) P_0, its
 // residual G - s X^T, and its P state G X - c P_0 (single-matrix groups: N = c, the pure
 // projection). c comes from the even reduction's per-item sums of squares of the matrix.
-template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PJ = false>
+// OE (odd-even pass, rank 1, world size 1, k_final_oe): the odd iteration k's rows as above, but
+// instead of storing the residual g - P x^T it accumulates the NEXT (even) iteration's raw
+// product: column partials sum_rows (g - P x^T) P over the row block (reference :185-202 for
+// iteration k + 1 with its in-factor P_k before the joint norm, which the reduction divides
+// out), and sum_rows P^2 for that norm. The gradient is read once for both iterations.
+template <typename T, int R, int K, int SMAX, bool VEC, int NT, int RB, bool PJ = false, bool OE = false>
 __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc& d, const Tile& t,
-                                               float* red, float* rqs = nullptr) {
+                                               float* red, float* rqs = nullptr, float* oered = nullptr) {
+    static_assert(!OE || (R == 1 && !PJ), "the odd-even pass is rank 1, K-term form");
     constexpr int KC = K > 0 ? K : 1;
     constexpr int NW = NT / 64;
     const int r = d.r;
@@ -231,6 +237,13 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
             for (int c = 0; c < R; ++c) o[v][c] = bq[k < KC ? k : 0][s][v][c];
     };
 
+    // OE: this thread's columns' partial of the next product, and (row-group leaders) sum P^2
+    float cacc[OE ? SMAX : 1][4];
+    float ssacc = 0.f;
+#pragma unroll
+    for (int s = 0; s < (OE ? SMAX : 1); ++s)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cacc[s][v] = 0.f;
     // segments past S load zeros (kOob) and drop their stores; their arithmetic is skipped
     // by a uniform branch
     auto seg_on = [&](int s) { return s < S; };
@@ -335,7 +348,8 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
                             }
                             a.yloc[e] = y;
                             a.state[e] = y;
-                            if constexpr (!PJ) {  // the exchange (W > 1) never takes the projection form
+                            if constexpr (OE) ssacc = fmaf(y, y, ssacc);
+                            if constexpr (!PJ && !OE) {  // the exchange (W > 1) never takes the projection form
                                 if (a.xout) st_slot(a.xout + e, y);
                             }
                         }
@@ -365,6 +379,14 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
 #pragma unroll
                             for (int k = 0; k < K; ++k) segb(k, s, bs[k]);
                         }
+                    }
+                    if constexpr (OE) {
+                        // the next iteration's raw product (rows past the block: P taken as 0,
+                        // so they add nothing whatever their error-feedback terms made of g)
+                        const float pv = valid ? pr[0] : 0.f;
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) cacc[s][v] = fmaf(g[u][s][v] - pv * xs[v][0], pv, cacc[s][v]);
+                        continue;
                     }
 #pragma unroll
                     for (int v = 0; v < 4; ++v) {
@@ -409,6 +431,32 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
         load(ga, b + 2);
         if (b + 1 < nb) process(gb, b + 1);
     }
+    if constexpr (OE) {
+        // the row groups' partials summed in row-group order (fixed), one [m] partial per block
+        float* ssl = oered + NT * SMAX * 4;
+#pragma unroll
+        for (int s = 0; s < SMAX; ++s)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) oered[((rg * Tg + tt) * SMAX + s) * 4 + v] = cacc[s][v];
+        if (tt == 0) ssl[rg] = ssacc;
+        __syncthreads();
+        if (rg == 0) {
+            float* part = a.oe_part + d.oe_part + int64_t(t.chunk) * m;
+#pragma unroll
+            for (int s = 0; s < SMAX; ++s)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    float sum = oered[(tt * SMAX + s) * 4 + v];
+                    for (int g2 = 1; g2 < RGS; ++g2) sum += oered[((g2 * Tg + tt) * SMAX + s) * 4 + v];
+                    if (act[s] && ccol[s] + v < m) part[ccol[s] + v] = sum;
+                }
+            if (tt == 0) {
+                float tot = ssl[0];
+                for (int g2 = 1; g2 < RGS; ++g2) tot += ssl[g2];
+                a.oe_ss[d.oe_blk0 + t.chunk] = tot;
+            }
+        }
+    }
 }
 
 template <typename T, int R, int K, int SMAX, bool PJ = false>
@@ -436,6 +484,21 @@ __device__ __forceinline__ void final_odd_block(const FinalArgs& a) {
 template <typename T, int R, int K, int SMAX>
 __global__ __launch_bounds__(FinNT<R>::value) void k_final_odd(FinalArgs a) {
     final_odd_block<T, R, K, SMAX, false>(a);
+}
+
+// Odd-even pass (rank 1, world size 1, an odd iteration followed by an even one inside a step:
+// I >= 3): the odd iteration's rows plus the next iteration's column partials, one gradient pass
+template <typename T, int K, int SMAX>
+__global__ __launch_bounds__(FinNT<1>::value) void k_final_oe(FinalArgs a) {
+    constexpr int NT = FinNT<1>::value, RB = FinRB<1>::value;
+    __shared__ float red[2 * (NT / 64) * RB];
+    __shared__ float oered[NT * SMAX * 4 + NT];
+    const Tile t = a.tiles[blockIdx.x];
+    const MatDesc d = a.mats[t.mat];
+    if (d.vec)
+        final_odd_tile<T, 1, K, SMAX, true, NT, RB, false, true>(a, d, t, red, nullptr, oered);
+    else
+        final_odd_tile<T, 1, K, SMAX, false, NT, RB, false, true>(a, d, t, red, nullptr, oered);
 }
 
 #ifndef PSGD_PROJ1_WPE
@@ -624,6 +687,41 @@ hipError_t dispatch_final(int R, int nres, int smax, const FinalArgs& a, int nti
         case 4: return dispatch_final_r<T, 4>(nres, smax, a, ntiles, s, waves);
         default: return hipErrorInvalidValue;
     }
+}
+
+template <typename T, int SMAX, int K>
+hipError_t launch_oe_k(const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    constexpr int NT = FinNT<1>::value;
+    if (waves) {  // resident waves per SIMD; 0 when the instance spills to scratch
+        const void* fn = reinterpret_cast<const void*>(&k_final_oe<T, K, SMAX>);
+        int blocks = 0;
+        hipFuncAttributes fa{};
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, NT, 0);
+        if (e == hipSuccess) e = hipFuncGetAttributes(&fa, fn);
+        if (e != hipSuccess) return e;
+        *waves = fa.localSizeBytes > 0 ? 0 : blocks * (NT / 64) / 4;
+    }
+    if (ntiles == 0) return hipSuccess;
+    k_final_oe<T, K, SMAX><<<ntiles, NT, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+// odd-even pass instances: SMAX buckets 2 / 3 / 5, earlier terms cached up to 3 (K = -1 beyond)
+template <typename T>
+hipError_t dispatch_final_oe(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    auto by_k = [&](auto SM) -> hipError_t {
+        constexpr int SMX = decltype(SM)::value;
+        switch (nres) {
+            case 1: return launch_oe_k<T, SMX, 1>(a, ntiles, s, waves);
+            case 2: return launch_oe_k<T, SMX, 2>(a, ntiles, s, waves);
+            case 3: return launch_oe_k<T, SMX, 3>(a, ntiles, s, waves);
+            default: return launch_oe_k<T, SMX, -1>(a, ntiles, s, waves);
+        }
+    };
+    if (smax <= 2) return by_k(std::integral_constant<int, 2>{});
+    if (smax <= 3) return by_k(std::integral_constant<int, 3>{});
+    if (smax <= 5) return by_k(std::integral_constant<int, 5>{});
+    return hipErrorInvalidValue;
 }
 
 template <typename T, int R>

@@ -59,6 +59,12 @@ struct MatDesc {
     int32_t fin_S;
     int32_t fin_rows;
     int32_t fin_rows_kt;
+    // odd-even pass (k_final_oe, rank 1, world size 1): row block b of the K-term geometry
+    // leaves its partial of the next even product at oe_part + b * m and its sum of P^2 at
+    // oe_ss[oe_blk0 + b]
+    int64_t oe_part;
+    int32_t oe_blk0;
+    int32_t oe_pad;
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.
@@ -269,7 +275,12 @@ struct FinalArgs {
     const int32_t* mrng_in;
     float* xout;           // one-shot exchange: P local also to this rank's exchange slot, or null
     int32_t out_nt;        // output stores nt only (large plans), else write-through (psgd_stream.cuh)
+    // odd-even pass (k_final_oe): no residual / output stores; per row block the next (even)
+    // iteration's raw product sum_rows (g - P x^T) P and sum_rows P^2 (MatDesc::oe_part / oe_blk0)
+    float* oe_part;
+    float* oe_ss;
 };
+hipError_t launch_final_oe(int dtype, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves);
 // nres value selecting the projection form of the fused final pass (I = 2, world size 1)
 constexpr int kFinProj = 1000;
 // rows per row block of the register-panel final pass (the projection form stages a block's

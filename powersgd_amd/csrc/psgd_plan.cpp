@@ -38,6 +38,12 @@ hipError_t launch_final_odd_bf16(int R, int nres, int smax, const FinalArgs& a, 
                                 int* waves);
 hipError_t launch_lowrank_out_f32(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_lowrank_out_bf16(int R, int nterms, const ApplyArgs& a, int ntiles, hipStream_t s);
+hipError_t launch_final_oe_f32(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves);
+hipError_t launch_final_oe_bf16(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves);
+hipError_t launch_final_oe(int dtype, int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
+    return dtype == PSGD_F32 ? launch_final_oe_f32(nres, smax, a, ntiles, s, waves)
+                             : launch_final_oe_bf16(nres, smax, a, ntiles, s, waves);
+}
 
 hipError_t launch_final_odd(int dtype, int R, int nres, int smax, const FinalArgs& a, int ntiles,
                             hipStream_t s, int* waves) {
@@ -367,6 +373,20 @@ struct psgd_plan {
     uint64_t dyn_base = 0;              // every pool head's value at the next launch
     size_t o_dyn = 0;                   // kDynPools heads, kDynStride apart (zeroed at bind)
     int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
+    // odd-even pass (k_final_oe: rank 1, world size 1, I >= 3): an odd iteration followed by an
+    // even one inside a step in ONE gradient pass; its partials (per K-term row block, [m]) are
+    // summed by k_reduce over red_oe, the blocks' sums of P^2 (oe_ss) give the even iteration's
+    // joint norm (grng_oe: per group its block range), and the items' sums of squares feed the
+    // next fused iteration (grng_oe_items: per group its red_oe range)
+    bool oe_ok = false;
+    std::vector<RedItem> red_oe;
+    std::vector<int32_t> grng_oe, grng_oe_items;
+    int64_t oe_part_floats = 0;
+    int32_t oe_blocks = 0;
+    size_t o_oe_part = 0, o_oe_ss = 0, o_red_oe = 0, o_grng_oe = 0, o_grng_oe_items = 0;
+    bool oe_at(int64_t step, int it, bool agg) const {  // iteration `it` runs the odd-even pass
+        return oe_ok && agg && it >= 1 && it + 1 < iters && !even(step, it);
+    }
     // reduction items (rebuilt with the geometry): even items follow the segmentation
     std::vector<RedItem> red_even, red_odd;
     std::vector<int32_t> grng_even, grng_odd;  // per group: [begin, end) of its reduction items
@@ -901,8 +921,43 @@ struct psgd_plan {
                 }
             }
         }
+        build_oe();
         build_reduction();
         if (!bucket_gend.empty()) build_spans();
+    }
+    void build_oe() {
+        oe_ok = false;
+        red_oe.clear();
+        grng_oe.assign(2 * groups.size(), 0);
+        grng_oe_items.assign(2 * groups.size(), 0);
+        oe_part_floats = 0;
+        oe_blocks = 0;
+        if (!fin_ok || rbucket != 1 || iters < 3 || f64() || env_int("PSGD_OE", 1) == 0) return;
+        int waves = 0;
+        FinalArgs none{};
+        if (launch_final_oe(dtype, iters - 2, fin_bucket(fin_smax), none, 0, nullptr, &waves) != hipSuccess || waves < 2)
+            return;
+        for (size_t i = 0; i < mats.size(); ++i) {
+            MatDesc& d = mats[i];
+            const int g = d.group;
+            const bool first = i == 0 || mats[i - 1].group != g;
+            if (first) {
+                grng_oe[2 * g] = oe_blocks;
+                grng_oe_items[2 * g] = int32_t(red_oe.size());
+            }
+            const int32_t nb = int32_t((d.n + d.fin_rows_kt - 1) / d.fin_rows_kt);
+            d.oe_blk0 = oe_blocks;
+            d.oe_part = oe_part_floats;
+            oe_blocks += nb;
+            oe_part_floats += int64_t(nb) * d.m;  // rank 1: [m] per block
+            const int pe = nb > kRedWide ? 1 : 4;
+            for (int64_t e = 0; e < d.m; e += 64 * pe)
+                red_oe.push_back(RedItem{int32_t(i), int32_t(e), pe, int32_t(std::min<int64_t>(64 * pe, d.m - e)),
+                                         d.oe_part + e, int32_t(d.m), nb});
+            grng_oe[2 * g + 1] = oe_blocks;
+            grng_oe_items[2 * g + 1] = int32_t(red_oe.size());
+        }
+        oe_ok = true;
     }
     // the last iteration of `step` runs fused (odd, and every matrix fits); `agg`: the caller
     // is psgd_aggregate (world size 1, output written), where the projection form also applies
@@ -996,6 +1051,12 @@ int psgd_plan::upload_tiles() const {
     if (qfold_ok)
         if (int st = upload(dev<void>(o_uitems), uitems.data(), uitems.size() * sizeof(int32_t))) return st;
     if (int st = upload(dev<void>(o_mrng), mrng_even.data(), mrng_even.size() * sizeof(int32_t))) return st;
+    if (oe_ok && o_red_oe) {
+        if (int st = upload(dev<void>(o_red_oe), red_oe.data(), red_oe.size() * sizeof(RedItem))) return st;
+        if (int st = upload(dev<void>(o_grng_oe), grng_oe.data(), grng_oe.size() * sizeof(int32_t))) return st;
+        if (int st = upload(dev<void>(o_grng_oe_items), grng_oe_items.data(), grng_oe_items.size() * sizeof(int32_t)))
+            return st;
+    }
     return PSGD_OK;
 }
 
@@ -1283,7 +1344,14 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_grng_even = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
     p->o_grng_odd = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
     p->o_mrng = carve(std::max<size_t>(2 * p->mats.size(), 1) * sizeof(int32_t));
-    p->ss_stride = size_t(std::max<int64_t>(p->red_even_cap, p->red_odd_cap));
+    p->ss_stride = size_t(std::max<int64_t>({p->red_even_cap, p->red_odd_cap, int64_t(p->red_oe.size())}));
+    if (p->oe_ok) {  // the odd-even pass's layout (geometry-independent: fixed at create)
+        p->o_oe_part = carve(size_t(p->oe_part_floats) * sizeof(float));
+        p->o_oe_ss = carve(size_t(std::max(p->oe_blocks, 1)) * sizeof(float));
+        p->o_red_oe = carve(std::max<size_t>(p->red_oe.size(), 1) * sizeof(RedItem));
+        p->o_grng_oe = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+        p->o_grng_oe_items = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
+    }
     p->o_ss = carve(2 * std::max<size_t>(p->ss_stride, 1) * sizeof(float));
     p->o_ss0 = carve(size_t(std::max<int64_t>(p->ss0_cap, 1)) * sizeof(float));
     p->o_grng_ss0 = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
@@ -1626,9 +1694,36 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     }
 
     // where the previous iteration's reduction left the per-item sums of squares of its
-    // out-factor (this iteration's raw in-factor) and the per-group item ranges
+    // out-factor (this iteration's raw in-factor) and the per-group item ranges (after an
+    // odd-even pass the previous even reduction ran over its own item list)
     const float* prev_ss = ss + size_t((it - 1) & 1) * p->ss_stride;
-    const int32_t* prev_grng = p->dev<int32_t>(even ? p->o_grng_odd : p->o_grng_even);
+    const bool oe_prev2 = !even && it >= 2 && p->oe_at(step, it - 2, write_out) && fused_norm(p, fuse, it - 2);
+    const int32_t* prev_grng = p->dev<int32_t>(even ? p->o_grng_odd : oe_prev2 ? p->o_grng_oe_items : p->o_grng_even);
+    // odd-even pass: this odd iteration and the next (even) one's product in one gradient pass
+    // (k_final_oe); its P rows need no reduction, the even iteration reduces its partials
+    if (fused && span == nullptr && p->oe_at(step, it, write_out)) {
+        FinalArgs fa{};
+        fa.mats = p->dev<MatDesc>(p->o_mats);
+        const bool own_kt = !p->tiles_fin_kt.empty();
+        fa.tiles = p->dev<Tile>(own_kt ? p->o_tiles_fin_kt : p->o_tiles_fin);
+        const int nfin = int(own_kt ? p->tiles_fin_kt.size() : p->tiles_fin.size());
+        fa.grads = p->grad_tab.table();
+        fa.x = p->hist(p->raw_slot, it - 1);
+        fill_terms(p, step, it, fa.res);
+        fa.nres = it;
+        fa.yloc = p->hist(1, it);
+        fa.state = out;
+        fa.ss_in = prev_ss;
+        fa.grng_in = prev_grng;
+        fa.xstate = in;
+        fa.hx = p->hist(0, it);
+        fa.ntiles = nfin;
+        fa.oe_part = p->dev<float>(p->o_oe_part);
+        fa.oe_ss = p->dev<float>(p->o_oe_ss);
+        PSGD_HIP(launch_final_oe(p->dtype, it, fin_bucket(p->fin_smax), fa, nfin, s, nullptr));
+        return PSGD_OK;
+    }
+    const bool oe_prev = even && it >= 1 && span == nullptr && p->oe_at(step, it - 1, write_out) && fused_norm(p, fuse, it - 1);
     if (it == p->iters - 1 && p->fused_final(step, write_out)) {
         // last iteration, odd: product + residual (+ output at world size 1) in one pass
         FinalArgs fa{};
@@ -1679,7 +1774,9 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     if (fused0) pa.ss0 = p->dev<float>(p->o_ss0);
     fill_terms(p, step, it, pa.res);
     pa.nres = it;
-    if (even) {
+    if (oe_prev) {
+        // the product of this even iteration was accumulated by the odd-even pass
+    } else if (even) {
         // persistent k_even: this span's workgroups [wg[0], wg[1]) of the segmentation
         pa.segs = p->dev<Seg>(p->o_segs);
         pa.wg_seg = p->dev<int32_t>(p->o_wg_seg) + sp.wg[0];
@@ -1711,6 +1808,11 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     ra.state = out;
     ra.even = even ? 1 : 0;
     ra.nmain = rr[1] - rr[0];
+    if (oe_prev) {  // the odd-even pass's block partials, per matrix [blocks][m]
+        ra.items = p->dev<RedItem>(p->o_red_oe);
+        ra.part = p->dev<float>(p->o_oe_part);
+        ra.nmain = int32_t(p->red_oe.size());
+    }
     if (fused0) {  // normalise the state P in place + history copy (P-side items)
         ra.ss_in = pa.ss0;
         ra.grng_in = p->dev<int32_t>(p->o_grng_ss0);
@@ -1721,8 +1823,8 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         ra.hx = p->hist(0, it);
     }
     if (fused) {  // in-factor items: the other parity's item list (in-factor side)
-        ra.ss_in = prev_ss;
-        ra.grng_in = prev_grng;
+        ra.ss_in = oe_prev ? p->dev<float>(p->o_oe_ss) : prev_ss;  // odd-even: the blocks' sums of P^2
+        ra.grng_in = oe_prev ? p->dev<int32_t>(p->o_grng_oe) : prev_grng;
         ra.nitems = p->dev<RedItem>(even ? p->o_red_odd : p->o_red_even) + rn[0];
         ra.nnorm = rn[1] - rn[0];
         ra.raw = p->hist(p->raw_slot, it - 1);
@@ -2078,6 +2180,14 @@ int psgd_plan_fused_final(const psgd_plan* p, int64_t step, int32_t aggregate, i
     if (!p || !fused) return fail(PSGD_ERR_VALUE, "null argument");
     if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
     *fused = p->proj_final(step, aggregate != 0) ? 2 : p->fused_final(step, aggregate != 0) ? 1 : 0;
+    return PSGD_OK;
+}
+
+int psgd_plan_odd_even(const psgd_plan* p, int64_t step, int32_t it, int32_t* on) {
+    if (!p || !on) return fail(PSGD_ERR_VALUE, "null argument");
+    if (step < 0 || it < 0 || it >= p->iters) return fail(PSGD_ERR_VALUE, "step/iteration out of range");
+    static const bool fuse = env_int("PSGD_FUSE_NORM", 1) != 0;  // as aggregate_impl
+    *on = p->oe_at(step, it, true) && fused_norm(p, fuse, it) ? 1 : 0;
     return PSGD_OK;
 }
 
