@@ -98,7 +98,7 @@ __device__ __forceinline__ void final_odd_tile(const FinalArgs& a, const MatDesc
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rg = tid / Tg, tt = tid - rg * Tg;
     const int RGS = NT / Tg;
-    const int64_t frows = PJ ? d.fin_rows : d.fin_rows_kt;
+    const int64_t frows = OE ? d.oe_rows : PJ ? d.fin_rows : d.fin_rows_kt;
     const int64_t row0 = int64_t(t.chunk) * frows;
     const int64_t row_end = d.n < row0 + frows ? d.n : row0 + frows;
     const int nres = K >= 0 ? K : a.nres;

@@ -59,12 +59,12 @@ struct MatDesc {
     int32_t fin_S;
     int32_t fin_rows;
     int32_t fin_rows_kt;
-    // odd-even pass (k_final_oe, rank 1, world size 1): row block b of the K-term geometry
-    // leaves its partial of the next even product at oe_part + b * m and its sum of P^2 at
-    // oe_ss[oe_blk0 + b]
+    // odd-even pass (k_final_oe, rank 1, world size 1): row block b (oe_rows rows, the K-term
+    // row-group geometry) leaves its partial of the next even product at oe_part + b * m and its
+    // sum of P^2 at oe_ss[oe_blk0 + b]
     int64_t oe_part;
     int32_t oe_blk0;
-    int32_t oe_pad;
+    int32_t oe_rows;
 };
 
 // Streaming tile: rows [chunk*chunk_rows, +chunk_rows) x columns of one strip.

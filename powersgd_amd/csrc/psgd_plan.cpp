@@ -380,10 +380,11 @@ struct psgd_plan {
     // next fused iteration (grng_oe_items: per group its red_oe range)
     bool oe_ok = false;
     std::vector<RedItem> red_oe;
+    std::vector<Tile> tiles_oe;  // its row blocks (MatDesc::oe_rows rows)
     std::vector<int32_t> grng_oe, grng_oe_items;
     int64_t oe_part_floats = 0;
     int32_t oe_blocks = 0;
-    size_t o_oe_part = 0, o_oe_ss = 0, o_red_oe = 0, o_grng_oe = 0, o_grng_oe_items = 0;
+    size_t o_oe_part = 0, o_oe_ss = 0, o_red_oe = 0, o_grng_oe = 0, o_grng_oe_items = 0, o_tiles_oe = 0;
     bool oe_at(int64_t step, int it, bool agg) const {  // iteration `it` runs the odd-even pass
         return oe_ok && agg && it >= 1 && it + 1 < iters && !even(step, it);
     }
@@ -928,6 +929,7 @@ struct psgd_plan {
     void build_oe() {
         oe_ok = false;
         red_oe.clear();
+        tiles_oe.clear();
         grng_oe.assign(2 * groups.size(), 0);
         grng_oe_items.assign(2 * groups.size(), 0);
         oe_part_floats = 0;
@@ -945,7 +947,11 @@ struct psgd_plan {
                 grng_oe[2 * g] = oe_blocks;
                 grng_oe_items[2 * g] = int32_t(red_oe.size());
             }
-            const int32_t nb = int32_t((d.n + d.fin_rows_kt - 1) / d.fin_rows_kt);
+            // PSGD_OE_ROWS: K-term row blocks per odd-even block (fewer, larger blocks: fewer
+            // partials for the reduction, fewer workgroups streaming)
+            d.oe_rows = int32_t(std::min<int64_t>(d.n, int64_t(d.fin_rows_kt) * std::max<int64_t>(1, env_int("PSGD_OE_ROWS", 1))));
+            const int32_t nb = int32_t((d.n + d.oe_rows - 1) / d.oe_rows);
+            for (int32_t b = 0; b < nb; ++b) tiles_oe.push_back(Tile{int32_t(i), 0, b, d.tensor});
             d.oe_blk0 = oe_blocks;
             d.oe_part = oe_part_floats;
             oe_blocks += nb;
@@ -1052,6 +1058,7 @@ int psgd_plan::upload_tiles() const {
         if (int st = upload(dev<void>(o_uitems), uitems.data(), uitems.size() * sizeof(int32_t))) return st;
     if (int st = upload(dev<void>(o_mrng), mrng_even.data(), mrng_even.size() * sizeof(int32_t))) return st;
     if (oe_ok && o_red_oe) {
+        if (int st = upload(dev<void>(o_tiles_oe), tiles_oe.data(), tiles_oe.size() * sizeof(Tile))) return st;
         if (int st = upload(dev<void>(o_red_oe), red_oe.data(), red_oe.size() * sizeof(RedItem))) return st;
         if (int st = upload(dev<void>(o_grng_oe), grng_oe.data(), grng_oe.size() * sizeof(int32_t))) return st;
         if (int st = upload(dev<void>(o_grng_oe_items), grng_oe_items.data(), grng_oe_items.size() * sizeof(int32_t)))
@@ -1347,6 +1354,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->ss_stride = size_t(std::max<int64_t>({p->red_even_cap, p->red_odd_cap, int64_t(p->red_oe.size())}));
     if (p->oe_ok) {  // the odd-even pass's layout (geometry-independent: fixed at create)
         p->o_oe_part = carve(size_t(p->oe_part_floats) * sizeof(float));
+        p->o_tiles_oe = carve(std::max<size_t>(p->tiles_oe.size(), 1) * sizeof(Tile));
         p->o_oe_ss = carve(size_t(std::max(p->oe_blocks, 1)) * sizeof(float));
         p->o_red_oe = carve(std::max<size_t>(p->red_oe.size(), 1) * sizeof(RedItem));
         p->o_grng_oe = carve(std::max<size_t>(2 * p->groups.size(), 1) * sizeof(int32_t));
@@ -1704,9 +1712,8 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
     if (fused && span == nullptr && p->oe_at(step, it, write_out)) {
         FinalArgs fa{};
         fa.mats = p->dev<MatDesc>(p->o_mats);
-        const bool own_kt = !p->tiles_fin_kt.empty();
-        fa.tiles = p->dev<Tile>(own_kt ? p->o_tiles_fin_kt : p->o_tiles_fin);
-        const int nfin = int(own_kt ? p->tiles_fin_kt.size() : p->tiles_fin.size());
+        fa.tiles = p->dev<Tile>(p->o_tiles_oe);
+        const int nfin = int(p->tiles_oe.size());
         fa.grads = p->grad_tab.table();
         fa.x = p->hist(p->raw_slot, it - 1);
         fill_terms(p, step, it, fa.res);

@@ -1854,8 +1854,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
                 }
         }
     } else {
+        // many partials per element (np > kRedWide, e.g. the odd-even pass's row blocks): 32 of
+        // a wave's partials in flight at once (two round trips where 16 took four on 256
+        // partials; the sum order is the same)
         const gptr<const float> p = pb + (lane < cnt ? lane : 0);
-        constexpr int kB = 16;
+        constexpr int kB = 32;
         for (int c = c0; c < c1; c += kB) {
             float v[kB];
 #pragma unroll
