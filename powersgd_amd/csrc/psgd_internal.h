@@ -199,6 +199,8 @@ struct ApplyArgs {
     // buffer (psgd_reconstruct)
     void* const* rdst;
     void* const* odst;
+    int32_t out_nt;      // world size 1 (shared terms): output stores nt only (large plans, as the
+                         // fused final pass's FinalArgs::out_nt), a separate kernel instance
 };
 
 struct ReduceArgs {

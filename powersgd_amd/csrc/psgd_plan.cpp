@@ -1882,6 +1882,7 @@ static int decompress_impl(psgd_plan* p, void* const* grads, void* out, int64_t 
     }
     aa.nterms = I;
     aa.alpha = float(1.0 / double(world));  // reference alpha = 1 / num_workers (:218)
+    aa.out_nt = world == 1 ? p->out_nt : 0;
     if (p->fused_final(step, false)) {
         // the residual was written by the fused last iteration: output only
         aa.ntiles = nt;

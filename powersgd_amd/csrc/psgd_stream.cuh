@@ -927,7 +927,7 @@ hipError_t dispatch_odd_mfma(int R, int nres, const ProductArgs& a, int ntiles, 
 }
 
 // ------------------------------------------------------------------ apply ---------
-template <typename T, int R, int NI, bool SHARED, int V>
+template <typename T, int R, int NI, bool SHARED, int V, bool ONT = false>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d, const Tile& t) {
     const TileGeom g = tile_geom<V>(d, t);
     const int r = d.r;
@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
             if (g.active && row + u * g.stride < g.row_end) {
                 const uint32_t off = uint32_t((b.rc[u] - g.row_begin) * g.m + g.col0) * uint32_t(sizeof(T));
                 st_vec<T>(rD, off, b.x[u]);
-                st_vec<T>(rO, off, o);
+                st_vec<T, ONT ? kStAuxOutNt : PSGD_ST_AUX>(rO, off, o);
             }
         }
     };
@@ -1042,7 +1042,10 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
     }
 }
 
-template <typename T, int R, int NI, bool SHARED>
+// ONT: the output stores nt only (world size 1, plans above PSGD_OUT_NT_MB: the averaged
+// gradient the optimizer reads next does not sit dirty in the Infinity Cache ahead of the next
+// step's cold reads); a compile-time instance, so the store form costs no registers
+template <typename T, int R, int NI, bool SHARED, bool ONT = false>
 __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
     // blocks [0, nitems): uncompressed tensors (first, so they run beside the first wave of
     // tiles rather than in the launch tail); then the tiles
@@ -1055,11 +1058,11 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
     const MatDesc d = a.mats[t.mat];
     if constexpr (R <= 8) {
         if (d.vec) {
-            apply_tile<T, R, NI, SHARED, 4>(a, d, t);
+            apply_tile<T, R, NI, SHARED, 4, ONT>(a, d, t);
             return;
         }
     }
-    apply_tile<T, R, NI, SHARED, 1>(a, d, t);
+    apply_tile<T, R, NI, SHARED, 1, ONT>(a, d, t);
 }
 
 // ------------------------------------------------------------------ dispatch ------
@@ -1108,7 +1111,9 @@ hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int nti
     const int NI = (kCache && nterms <= maxni) ? nterms : -1;
 #define PSGD_A(NN)                                                                       \
     do {                                                                                 \
-        if (shared)                                                                      \
+        if (shared && a.out_nt)                                                          \
+            timed_launch(&k_apply<T, R, NN, true, true>, grid, block, s, a);             \
+        else if (shared)                                                                 \
             timed_launch(&k_apply<T, R, NN, true>, grid, block, s, a);                   \
         else                                                                             \
             timed_launch(&k_apply<T, R, NN, false>, grid, block, s, a);                  \
