@@ -171,10 +171,15 @@ int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64
  * peer that never arrives sets the status word read by psgd_ipc_status instead of hanging).
  * No host barrier and no host synchronisation per step.
  *   psgd_ipc_create   allocates this rank's exchange buffer (flags + two parities x iterations
- *                     slots, room for flat_numel uncompressed values) and exports its handle
- *                     (psgd_ipc_handle_bytes bytes). Synchronous.
+ *                     slots, room for flat_numel uncompressed values), draws a fresh session
+ *                     nonce into its header and exports handle + nonce (psgd_ipc_handle_bytes
+ *                     bytes). Synchronous.
  *   psgd_ipc_open     the caller all-gathers the W handles (e.g. torch.distributed) and passes
- *                     them in rank order; opens the peers' buffers.
+ *                     them in rank order; opens the peers' buffers and reads each peer's nonce
+ *                     through the mapping: a mapping that does not reach that session's buffer
+ *                     (stale) is PSGD_ERR_STATE, a list whose own entry is not this rank's handle
+ *                     PSGD_ERR_VALUE. Every epoch flag carries its writer's nonce in the high
+ *                     32 bits and pollers accept only the nonce they opened with.
  *   psgd_aggregate_ipc the whole step on `stream` (same arguments as psgd_aggregate_comm).
  *   psgd_ipc_status   synchronous: 1 if a wait timed out since the last call (results invalid).
  *   psgd_ipc_close    synchronous: unmap the peers. Teardown is collective: every rank calls it,

@@ -387,7 +387,13 @@ constexpr int64_t kXchgHeader = 256;
 // byte offset, in the header, of the device copy of the sticky error word (XchgArgs::err_dev):
 // past the flags of every iteration (num_iters_per_step <= kMaxTerms)
 constexpr int64_t kXchgErrOff = 192;
-static_assert(kMaxTerms * 8 <= kXchgErrOff && kXchgErrOff + 4 <= kXchgHeader, "exchange header layout");
+// byte offset of this buffer's session nonce (uint32, written at psgd_ipc_create): peers check it
+// through their mapping at psgd_ipc_open, and every epoch flag carries it in its high word, so a
+// mapping that does not reach THIS session's buffer (a runtime that hands back a stale mapping
+// of a freed buffer with an identical handle) fails loudly instead of summing stale slots
+constexpr int64_t kXchgNonceOff = 200;
+static_assert(kMaxTerms * 8 <= kXchgErrOff && kXchgErrOff + 4 <= kXchgNonceOff && kXchgNonceOff + 4 <= kXchgHeader,
+              "exchange header layout");
 struct XchgArgs {
     const char* const* peers;  // device array: the W exchange buffers (rank order, own included)
     uint64_t* own_flag;        // this rank's flag of this iteration (its own buffer)
@@ -398,7 +404,9 @@ struct XchgArgs {
     float* flat_dst;           // SUM of the packed uncompressed tensors (last iteration) ...
     int64_t flat_off;          // ... at slot + flat_off floats
     int64_t nflat;
-    uint64_t epoch;            // step + 1
+    uint64_t epoch;            // step + 1 (< 2^32)
+    const uint32_t* nonces;    // device array: every rank's session nonce (flag = nonce << 32 | epoch)
+    uint32_t own_nonce;
     uint32_t spin_limit;       // polls (~0.25 us apart) before a wait gives up
     int32_t world, rank;
     int32_t* err;              // set to 1 when a wait timed out (psgd_ipc_status; host-mapped)

@@ -9,6 +9,9 @@
 //   - iteration parity = (step * num_iters_per_step + it) % 2 (:174).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+#include <unistd.h>
 #include <algorithm>
 #include <cmath>
 #include <cassert>
@@ -494,7 +497,8 @@ struct psgd_plan {
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
     int64_t ipc_slot = 0, ipc_flat_off = 0, ipc_flat_cap = 0;
-    size_t o_ipc_ptrs = 0;
+    size_t o_ipc_ptrs = 0, o_ipc_nonce = 0;
+    uint32_t ipc_nonce = 0;  // this rank's exchange session (psgd_ipc_create)
     // sticky timeout word of the exchange waits: pinned host memory mapped into the device
     // (k_xchg stores 1 with a system-scope store), so every psgd_aggregate_ipc call can check it
     // without synchronising; cleared only by psgd_ipc_close
@@ -1345,6 +1349,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_munits_p = carve(p->munits_p.size() * sizeof(OrthUnit));
     p->o_munits_q = carve(p->munits_q.size() * sizeof(OrthUnit));
     p->o_ipc_ptrs = carve(size_t(kMaxRanks) * sizeof(void*));
+    p->o_ipc_nonce = carve(size_t(kMaxRanks) * sizeof(uint32_t));
     p->o_rq = carve(size_t(std::max<int64_t>(p->fmax, 1)) * sizeof(float));
     p->o_rdst = carve(TableCache::bytes(size_t(num_tensors)));
     p->o_odst = carve(TableCache::bytes(size_t(num_tensors)));
@@ -1979,9 +1984,12 @@ int psgd_decompress_bucket(psgd_plan* p, void* const* grads, void* out, int64_t 
 }
 
 // ------------------------------------------------- one-shot all-reduce over IPC ---
+// an exchange handle: the HIP IPC handle of the buffer, then the buffer's session nonce
+constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t) + sizeof(uint32_t);
+
 int psgd_ipc_handle_bytes(int64_t* bytes) {
     if (!bytes) return fail(PSGD_ERR_VALUE, "null argument");
-    *bytes = int64_t(sizeof(hipIpcMemHandle_t));
+    *bytes = int64_t(kHandleBytes);
     return PSGD_OK;
 }
 
@@ -2005,8 +2013,20 @@ int psgd_ipc_create(psgd_plan* p, int64_t flat_numel, void* handle_out) {
         PSGD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p->xerr_dev), p->xerr_host, 0));
     }
     __atomic_store_n(p->xerr_host, 0, __ATOMIC_RELEASE);
+    // a fresh session nonce (never 0: a zeroed header never matches), in the header and the handle
+    {
+        static std::atomic<uint32_t> counter{0};
+        uint64_t z = uint64_t(std::chrono::steady_clock::now().time_since_epoch().count()) ^
+                     (uint64_t(reinterpret_cast<uintptr_t>(p->ipc_buf)) << 7) ^ (uint64_t(getpid()) << 40) ^
+                     (uint64_t(counter.fetch_add(1)) * 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p->ipc_nonce = uint32_t(z ^ (z >> 31)) | 1u;
+    }
+    PSGD_HIP(hipMemcpy(p->ipc_buf + kXchgNonceOff, &p->ipc_nonce, sizeof(uint32_t), hipMemcpyHostToDevice));
     PSGD_HIP(hipDeviceSynchronize());  // zeroed before any peer can open and poll it
     PSGD_HIP(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), p->ipc_buf));
+    std::memcpy(static_cast<char*>(handle_out) + sizeof(hipIpcMemHandle_t), &p->ipc_nonce, sizeof(uint32_t));
     return PSGD_OK;
 }
 
@@ -2016,23 +2036,45 @@ int psgd_ipc_open(psgd_plan* p, int32_t world, int32_t rank, const void* handles
     if (!p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "peers already open (psgd_ipc_close first)");
     if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return fail(PSGD_ERR_VALUE, "bad world/rank");
     DevScope scope(p->device);
-    const auto* h = static_cast<const hipIpcMemHandle_t*>(handles);
+    const char* hb = static_cast<const char*>(handles);
     std::vector<void*> peer(size_t(world), nullptr);
+    std::vector<uint32_t> nonce(size_t(world), 0);
+    auto close_open = [&](int upto) {
+        for (int v = 0; v < upto; ++v)
+            if (v != rank && peer[v]) (void)hipIpcCloseMemHandle(peer[v]);
+    };
     for (int w = 0; w < world; ++w) {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, hb + size_t(w) * kHandleBytes, sizeof(h));
+        std::memcpy(&nonce[w], hb + size_t(w) * kHandleBytes + sizeof(h), sizeof(uint32_t));
         if (w == rank) {
             peer[w] = p->ipc_buf;
+            if (nonce[w] != p->ipc_nonce) {
+                close_open(w);
+                return fail(PSGD_ERR_VALUE, "handle list: this rank's entry is not its own exchange handle");
+            }
             continue;
         }
-        const hipError_t e = hipIpcOpenMemHandle(&peer[w], h[w], hipIpcMemLazyEnablePeerAccess);
+        const hipError_t e = hipIpcOpenMemHandle(&peer[w], h, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess) {
-            for (int v = 0; v < w; ++v)
-                if (v != rank && peer[v]) (void)hipIpcCloseMemHandle(peer[v]);
+            close_open(w);
             return fail(PSGD_ERR_DEVICE, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        }
+        // the mapping must reach THIS session's buffer of rank w: its header carries the nonce the
+        // handle announced (a stale mapping of an earlier, freed buffer does not)
+        uint32_t seen = 0;
+        const hipError_t e2 = hipMemcpy(&seen, static_cast<char*>(peer[w]) + kXchgNonceOff, sizeof(uint32_t),
+                                        hipMemcpyDeviceToHost);
+        if (e2 != hipSuccess || seen != nonce[w]) {
+            close_open(w + 1);
+            return fail(PSGD_ERR_STATE, "the mapping of rank " + std::to_string(w) +
+                                            "'s exchange buffer does not reach this session's buffer (stale IPC mapping)");
         }
     }
     p->ipc_peer = peer;
     p->ipc_world = world;
     p->ipc_rank = rank;
+    if (int st = upload(p->dev<void>(p->o_ipc_nonce), nonce.data(), size_t(world) * sizeof(uint32_t))) return st;
     return upload(p->dev<void>(p->o_ipc_ptrs), p->ipc_peer.data(), size_t(world) * sizeof(void*));
 }
 
@@ -2507,7 +2549,7 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
     if (p->xerr_set())
         return fail(PSGD_ERR_STATE, "an earlier IPC exchange wait timed out (a peer did not arrive within "
                                     "PSGD_IPC_SPIN); the exchange is invalid until psgd_ipc_close");
-    if (step < 0) return fail(PSGD_ERR_VALUE, "step out of range");
+    if (step < 0 || step >= 0xffffffffLL) return fail(PSGD_ERR_VALUE, "step out of range (epochs are 32-bit)");
     if (reinterpret_cast<uintptr_t>(out) % 16) return fail(PSGD_ERR_LAYOUT, "output buffer must be 16-byte aligned");
     const bool has_flat = f && f->total > 0;
     if (has_flat) {
@@ -2577,6 +2619,8 @@ int psgd_aggregate_ipc(psgd_plan* p, void* const* grads, void* out, int64_t step
             xa.nflat = f->total;
         }
         xa.epoch = uint64_t(step) + 1;
+        xa.nonces = p->dev<const uint32_t>(p->o_ipc_nonce);
+        xa.own_nonce = p->ipc_nonce;
         xa.spin_limit = spin;
         xa.world = world;
         xa.rank = p->ipc_rank;

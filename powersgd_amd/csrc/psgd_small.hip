@@ -2000,10 +2000,12 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
     // the slot bytes were written through by the PREVIOUS kernels of this stream (steps 1-2
     // above): the flag is a plain system-scope store, no fence
     if (blockIdx.x == 0 && tid == 0)
-        __hip_atomic_store(a.own_flag, a.epoch, PSGD_XCHG_FLAG_ORDER, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.own_flag, (uint64_t(a.own_nonce) << 32) | a.epoch, PSGD_XCHG_FLAG_ORDER,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
     bool dead = false;
     if (tid < a.world && tid != a.rank) {  // lane w polls peer w: the W round trips overlap
         const uint64_t* f = reinterpret_cast<const uint64_t*>(a.peers[tid] + a.flag_off);
+        const uint32_t want = a.nonces[tid];  // this session's flags only
         uint32_t spins = 0;
         for (;;) {
             // the device copy of the sticky error word, loaded beside the flag (no extra round
@@ -2015,7 +2017,7 @@ __global__ __launch_bounds__(kBlock) void k_xchg(XchgArgs a) {
                 dead = true;
                 break;
             }
-            if (fv >= a.epoch) break;
+            if (uint32_t(fv >> 32) == want && (fv & 0xffffffffull) >= a.epoch) break;
             if (++spins > a.spin_limit) {
                 // host-mapped sticky word (vector store, system scope) and its device copy: the
                 // results of this step are invalid and the host refuses every later exchange step

@@ -4,6 +4,7 @@ all-reduce of a step (and the uncompressed tensors) is a device-side flag handsh
 rank-order sum, with no host barrier or synchronisation per step (gloo carries only the one-off
 handle exchange). Checked against the reference's own multi-worker goldens (F2), like the
 collective path; plus skewed ranks and the bounded wait."""
+import gc
 import os
 import tempfile
 import time
@@ -19,42 +20,48 @@ MAN = manifest()
 TOL_FREE = 1e-4
 
 
-def _worker(rank_id, world, key, initfile, skew):
+def _worker(rank_id, world, key, initfile, skew, sessions=1):
     os.environ["PSGD_COMM"] = "ipc"
-    from powersgd_amd import Config, PowerSGD
-
     torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id, world_size=world)
     try:
-        info = MAN["multi"][key]
-        meta = MAN["scenarios"][info["scenario"]]
-        want = load("F2_" + key)
-        pre = f"rank{rank_id}_"
-        dev = torch.device("cuda:0")
-        shapes = [tuple(s) for s in meta["shapes"]]
-        psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes],
-                        Config(meta["rank"], meta["mcr"], meta["iters"], meta["start"]))
-        psgd._powersgd._ps_buffer.copy_(torch.from_numpy(want[pre + "p0"]).to(dev))
-        psgd._powersgd._qs_buffer.copy_(torch.from_numpy(want[pre + "q0"]).to(dev))
-        res = [torch.zeros(s) for s in shapes]
-        for t in range(meta["steps"]):
-            inputs = scenario_inputs(meta, t, res, rank_id)
-            grads = [g.to(dev) for g in inputs]
-            if skew and rank_id == t % world:
-                time.sleep(0.3)  # this rank arrives late: the peers' kernels wait on its flags
-            outs = psgd.aggregate(grads)
-            torch.cuda.synchronize()
-            for i, g in enumerate(inputs):
-                scale = max(float(g.norm()), 1e-30)
-                eo = float((outs[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_out_{i}"])).norm()) / scale
-                er = float((grads[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_res_{i}"])).norm()) / scale
-                check(eo, TOL_FREE, key, rank_id, t, i, "ipc-out")
-                check(er, TOL_FREE, key, rank_id, t, i, "ipc-res")
-            res = [g.cpu() for g in grads]
-        assert psgd._powersgd._ipc_open
-        assert not psgd._powersgd.ipc_status(), "a device-side exchange wait timed out"
-        psgd._powersgd.close_ipc()
+        for _ in range(sessions):
+            _session(rank_id, world, key, skew)
+            gc.collect()  # the codec (and its exchange buffer) is freed before the next one is made
     finally:
         torch.distributed.destroy_process_group()
+
+
+def _session(rank_id, world, key, skew):
+    from powersgd_amd import Config, PowerSGD
+
+    info = MAN["multi"][key]
+    meta = MAN["scenarios"][info["scenario"]]
+    want = load("F2_" + key)
+    pre = f"rank{rank_id}_"
+    dev = torch.device("cuda:0")
+    shapes = [tuple(s) for s in meta["shapes"]]
+    psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes],
+                    Config(meta["rank"], meta["mcr"], meta["iters"], meta["start"]))
+    psgd._powersgd._ps_buffer.copy_(torch.from_numpy(want[pre + "p0"]).to(dev))
+    psgd._powersgd._qs_buffer.copy_(torch.from_numpy(want[pre + "q0"]).to(dev))
+    res = [torch.zeros(s) for s in shapes]
+    for t in range(meta["steps"]):
+        inputs = scenario_inputs(meta, t, res, rank_id)
+        grads = [g.to(dev) for g in inputs]
+        if skew and rank_id == t % world:
+            time.sleep(0.3)  # this rank arrives late: the peers' kernels wait on its flags
+        outs = psgd.aggregate(grads)
+        torch.cuda.synchronize()
+        for i, g in enumerate(inputs):
+            scale = max(float(g.norm()), 1e-30)
+            eo = float((outs[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_out_{i}"])).norm()) / scale
+            er = float((grads[i].cpu() - torch.from_numpy(want[f"{pre}s{t}_res_{i}"])).norm()) / scale
+            check(eo, TOL_FREE, key, rank_id, t, i, "ipc-out")
+            check(er, TOL_FREE, key, rank_id, t, i, "ipc-res")
+        res = [g.cpu() for g in grads]
+    assert psgd._powersgd._ipc_open
+    assert not psgd._powersgd.ipc_status(), "a device-side exchange wait timed out"
+    psgd._powersgd.close_ipc()
 
 
 @pytest.mark.parametrize("key", sorted(MAN["multi"]))
@@ -71,6 +78,54 @@ def test_ipc_skewed_ranks():
     key = sorted(k for k in MAN["multi"] if MAN["multi"][k]["world"] == 2)[0]
     with tempfile.TemporaryDirectory() as td:
         torch.multiprocessing.spawn(_worker, args=(2, key, os.path.join(td, "init"), True), nprocs=2, join=True)
+
+
+def test_ipc_sessions_back_to_back():
+    """Three codecs of the same shapes one after the other in the same processes, each freed
+    before the next is made: every session's exchange buffer is a fresh allocation of the same
+    size, its mappings are verified against the session nonce at open, and every session still
+    matches the reference goldens step by step."""
+    key = sorted(k for k in MAN["multi"] if MAN["multi"][k]["world"] == 2)[0]
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_worker, args=(2, key, os.path.join(td, "init"), False, 3), nprocs=2,
+                                    join=True)
+
+
+def _nonce_worker(rank_id, initfile):
+    from powersgd_amd import Config, PowerSGD
+
+    torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id, world_size=2)
+    try:
+        dev = torch.device("cuda:0")
+        psgd = PowerSGD([torch.zeros(64, 32, device=dev)], Config(2, 1, 2, 0))
+        plan = psgd._powersgd._plan
+        h = plan.ipc_create(0)
+        hs = [None, None]
+        torch.distributed.all_gather_object(hs, h)
+        peer = 1 - rank_id
+        # negative control: the peer's handle announces another session's nonce than the one its
+        # buffer holds (what a stale mapping of an earlier buffer looks like): the open refuses
+        bad = list(hs)
+        nonce = int.from_bytes(bad[peer][-4:], "little")
+        bad[peer] = bad[peer][:-4] + (nonce ^ 0x10).to_bytes(4, "little")
+        with pytest.raises(RuntimeError, match="stale IPC mapping"):
+            plan.ipc_open(2, rank_id, bad)
+        # this rank's own entry must be its own handle
+        own = list(hs)
+        own[rank_id] = own[rank_id][:-4] + (int.from_bytes(own[rank_id][-4:], "little") ^ 0x10).to_bytes(4, "little")
+        with pytest.raises(ValueError, match="own exchange handle"):
+            plan.ipc_open(2, rank_id, own)
+        plan.ipc_open(2, rank_id, hs)  # the true list opens
+        torch.distributed.barrier()
+        plan.ipc_close()
+        torch.distributed.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_ipc_open_checks_session_nonce():
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_nonce_worker, args=(os.path.join(td, "init"),), nprocs=2, join=True)
 
 
 def _timeout_worker(rank_id, initfile):
