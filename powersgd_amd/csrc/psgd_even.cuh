@@ -36,6 +36,12 @@ namespace psgd {
 #ifndef PSGD_EVEN_U_BF16
 #define PSGD_EVEN_U_BF16 PSGD_EVEN_U
 #endif
+// rank 4, narrow strips (V = 4, fewer than 64 lanes per row): rows in flight per lane. 3 keeps
+// the rank-4 instance at 80 VGPRs (6 waves per SIMD: 3 workgroups per CU instead of 2); its
+// full-width path alone needs 70. cfg3 k_even 23.06 -> 22.4 us (profiles/r05/even_occ)
+#ifndef PSGD_EVEN_U_NR4
+#define PSGD_EVEN_U_NR4 3
+#endif
 constexpr int kEvenNT = PSGD_EVEN_NT;
 constexpr int kEvenNW = kEvenNT / 64;
 constexpr int kEvenU = PSGD_EVEN_U;
@@ -262,7 +268,7 @@ template <typename T, int R, int K, int V>
 __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, const void* gp, float* red,
                                          float* ssl) {
     constexpr uint32_t s = sizeof(T);
-    constexpr int U = R <= 8 ? kEvenU : R == 16 ? 2 : 1;  // fewer rows in flight at ranks 16/32
+    constexpr int U = (R == 4 && V == 4) ? PSGD_EVEN_U_NR4 : R <= 8 ? kEvenU : R == 16 ? 2 : 1;  // fewer rows in flight at ranks 16/32
     const int tid = threadIdx.x, lane = tid & 63, wave = uni(int32_t(tid >> 6));
     const int L = sg.lanes, rw = 64 / L;
     const int sub = lane / L, ql = lane - sub * L;
@@ -372,7 +378,7 @@ __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, co
 #define PSGD_EVEN_WPE_R2 6
 #endif
 #ifndef PSGD_EVEN_WPE_R4
-#define PSGD_EVEN_WPE_R4 5
+#define PSGD_EVEN_WPE_R4 6
 #endif
 // bf16 gradients: the narrow-strip paths' 16-bit loads and conversions need more registers; at
 // the fp32 targets the rank-2/4 instances spilled VGPRs to scratch (tools/regs.py), so one wave
@@ -491,6 +497,24 @@ hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg0, hipStream_t
         k_even<T, R, -1><<<grid, block, 0, s>>>(a);
     }
     return hipGetLastError();
+}
+
+// workgroups of the first-iteration instance (K = 0, static ranges) resident per CU: the plan's
+// default workgroups per CU, so that the whole grid is one wave of resident workgroups (measured:
+// rank 4 fp32 3 per CU 22.0 us against 22.7 at 4; bf16 rank 2 2 per CU 24.6 against 28.0;
+// profiles/r05/even_occ)
+template <typename T>
+int even_resident(int R) {
+    int n = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (R) {
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 1, 0>, kEvenNT, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 2, 0>, kEvenNT, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 4, 0>, kEvenNT, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 8, 0>, kEvenNT, 0); break;
+        default: break;
+    }
+    return e == hipSuccess ? n : 0;
 }
 
 template <typename T>

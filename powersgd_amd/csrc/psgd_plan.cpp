@@ -29,6 +29,8 @@
 namespace psgd {
 hipError_t launch_even_f32(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s);
 hipError_t launch_even_bf16(int R, int nres, const ProductArgs& a, int nwg, hipStream_t s);
+int even_resident_f32(int R);
+int even_resident_bf16(int R);
 hipError_t launch_product_odd_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_product_odd_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s);
 hipError_t launch_apply_f32(int R, int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s);
@@ -1203,7 +1205,14 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
                                                             : std::min<int64_t>(65536, std::max<int64_t>(4096, total / 1536));
         p->fin_elems_kt = std::max<int64_t>(1024, env_int("PSGD_FIN_ELEMS_KT", env_int("PSGD_FIN_ELEMS", dflt_kt)));
         // persistent even product: workgroups per CU, minimum gradient elements per workgroup
-        p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", 4))));
+        // default: the first-iteration instance's resident workgroups per CU (capped at 4), so the
+        // grid is one wave of resident workgroups (rank 4: 3 since the narrow-strip path fits 6
+        // waves per SIMD; bf16 ranks 2 / 4: 2)
+        int resident = p->rbucket <= 8 ? (p->dtype == PSGD_F32 ? even_resident_f32(p->rbucket)
+                                                                : even_resident_bf16(p->rbucket))
+                                       : 0;
+        resident = resident > 0 ? std::min(resident, 4) : 4;
+        p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", resident))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
         p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
         // ranges per workgroup (dynamic assignment); the ranges of a launch stay within the

@@ -11,4 +11,5 @@ hipError_t launch_product_odd_bf16(int R, int nres, const ProductArgs& a, int nt
 hipError_t launch_odd_mfma_bf16(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     return dispatch_odd_mfma<bf16_t>(R, nres, a, ntiles, s);
 }
+int even_resident_bf16(int R) { return even_resident<bf16_t>(R); }
 }  // namespace psgd

@@ -11,4 +11,5 @@ hipError_t launch_product_odd_f32(int R, int nres, const ProductArgs& a, int nti
 hipError_t launch_odd_mfma_f32(int R, int nres, const ProductArgs& a, int ntiles, hipStream_t s) {
     return dispatch_odd_mfma<float>(R, nres, a, ntiles, s);
 }
+int even_resident_f32(int R) { return even_resident<float>(R); }
 }  // namespace psgd

@@ -300,3 +300,40 @@ def test_even_segmentation_forms(rank, wpc, emin, dyn):
             check(_rel(gd[i], gc[i], g), tol, rank, wpc, emin, dyn, i, "res")
     for x, y in zip(runs[0], runs[1]):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("rank,dt", [(2, torch.float32), (4, torch.float32), (2, torch.bfloat16),
+                                     (4, torch.bfloat16)])
+def test_even_full_width_plans(rank, dt):
+    """Ranks 2 / 4, fp32 and bf16, at the default k_even workgroups per CU (the instance's
+    resident count: 3 at rank 4 fp32, 2 for bf16 rank 2): plans whose every matrix is
+    full-width strips (a ragged column count, 700, leaves a partial last strip; a tall-thin
+    matrix), then with one narrow matrix added (the narrow-strip path with 3 rows in flight at
+    rank 4). One step against the oracle from the same state, and a bitwise rerun."""
+    for shapes in ([(512, 1024), (300, 700), (2048, 256)], [(512, 1024), (300, 700), (2048, 256), (96, 40)]):
+        psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dt) for s in shapes], Config(rank, 2, 2, 0))
+        p0 = psgd._powersgd._ps_buffer.clone()
+        q0 = psgd._powersgd._qs_buffer.clone()
+        new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=91)]
+        gin = [g.to(DEV).to(dt) for g in new]
+        ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 2, 2, 0)
+        ora.codec.p_flat.copy_(p0.cpu())
+        ora.codec.q_flat.copy_(q0.cpu())
+        gc = [g.float().cpu() for g in gin]
+        scale = [g.clone() for g in gc]
+        oc = O.policy_step(ora, gc)
+        runs = []
+        for _ in range(2):
+            psgd._powersgd._ps_buffer.copy_(p0)
+            psgd._powersgd._qs_buffer.copy_(q0)
+            psgd.step_counter = psgd._powersgd.step_counter = 0
+            gd = [g.clone() for g in gin]
+            od = psgd.aggregate(gd)
+            torch.cuda.synchronize()
+            runs.append([o.clone() for o in od] + [g.clone() for g in gd])
+            tol = TOL_BF16 if dt == torch.bfloat16 else TOL_STEP
+            for i, g in enumerate(scale):
+                check(_rel(od[i].float(), oc[i], g), tol, rank, str(dt), len(shapes), i, "out")
+                check(_rel(gd[i].float(), gc[i], g), tol, rank, str(dt), len(shapes), i, "res")
+        for x, y in zip(runs[0], runs[1]):
+            assert torch.equal(x, y)
