@@ -1,6 +1,6 @@
 """Plain world-size-1 steps of one config (no timing events, no other blocks): run under
 rocprofv3 --kernel-trace to see a step's kernel sequence and its launch gaps as the bench's
-timed loop runs them. usage: python tools/step_trace.py <config> [steps]"""
+timed loop runs them. usage: python tools/step_trace.py <config> [steps] [rank override]"""
 import sys
 
 import torch
@@ -12,7 +12,9 @@ from powersgd_amd.workloads import CONFIGS  # noqa: E402
 cfg = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 dev = torch.device("cuda:0")
-c = CONFIGS[cfg]
+c = dict(CONFIGS[cfg])
+if len(sys.argv) > 3:
+    c["rank"] = int(sys.argv[3])
 dtype = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
 gen = torch.Generator(device=dev).manual_seed(1)
 sets = [[torch.randn(s, generator=gen, device=dev).to(dtype) for s in c["shapes"]] for _ in range(4)]
