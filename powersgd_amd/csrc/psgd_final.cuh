@@ -25,9 +25,8 @@ namespace psgd {
 
 // Rows per row group per batch (each batch double-buffered: the next batch's loads are in
 // flight while this one reduces and stores): 1 (ranks 1/2: 2 measured 0.6-2 us slower on the
-// ResNet-50 and Llama final passes, profiles/r03/v, profiles/r03/x; fewer registers per row). Workgroup size: 512
-// threads at rank 4 (a row spread over twice the threads keeps the per-thread factor
-// panels, S * 4 * r floats each, within two waves per SIMD), else 256.
+// ResNet-50 and Llama final passes, profiles/r03/v, profiles/r03/x; fewer registers per row). Workgroup size: 256
+// threads (rank 4: PSGD_FIN_NT4 below).
 #ifndef PSGD_FIN_RB12
 #define PSGD_FIN_RB12 1
 #endif
@@ -35,9 +34,20 @@ template <int R>
 struct FinRB {
     static constexpr int value = R == 4 ? 1 : PSGD_FIN_RB12;
 };
+// rank 4: PSGD_FIN_NT4 threads per workgroup. 256 with up to 5 register segments per thread
+// (187 VGPRs, 2 waves per SIMD; PSGD_PROJ4_WPE) against 512 with 3 (128 VGPRs, 4 waves per
+// SIMD): fewer idle lanes on the 9c-column rows (4608 columns: 1280 slots for 1152 quads
+// instead of 1536), cfg3 k_final_proj 53.9-54.6 -> 51.7-52.5 us, step 0.0938-0.0941 -> 0.0923-
+// 0.0925 ms (profiles/r05/fin_nt4). At 3 waves per SIMD the instance spills (168 + 29 VGPRs)
+#ifndef PSGD_FIN_NT4
+#define PSGD_FIN_NT4 256
+#endif
+#ifndef PSGD_PROJ4_WPE
+#define PSGD_PROJ4_WPE 2
+#endif
 template <int R>
 struct FinNT {
-    static constexpr int value = R == 4 ? 512 : 256;
+    static constexpr int value = R == 4 ? PSGD_FIN_NT4 : 256;
 };
 
 // Gradient / output rows go through buffer descriptors spanning exactly one matrix: a
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(FinNT<1>::value) void k_final_oe(FinalArgs a) {
 // Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
 // CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
 template <typename T, int R, int SMAX>
-__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? 4 : R == 1 ? PSGD_PROJ1_WPE : 1))) void k_final_proj(
+__global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? PSGD_PROJ4_WPE : R == 1 ? PSGD_PROJ1_WPE : 1))) void k_final_proj(
     FinalArgs a) {
     final_odd_block<T, R, 0, SMAX, true>(a);
 }
@@ -667,6 +677,9 @@ template <typename T, int R>
 hipError_t dispatch_final_r(int nres, int smax, const FinalArgs& a, int ntiles, hipStream_t s, int* waves) {
     if (smax <= 2) return dispatch_final_k<T, R, 2>(nres, a, ntiles, s, waves);
     if (smax <= 3) return dispatch_final_k<T, R, 3>(nres, a, ntiles, s, waves);
+    if constexpr (R == 4 && PSGD_FIN_NT4 == 256) {
+        if (smax <= 5 && nres == kFinProj) return launch_final_k<T, R, 5, 0, true>(a, ntiles, s, waves);
+    }
     if constexpr (R <= 2) {
         if (smax <= 5) return dispatch_final_k<T, R, 5>(nres, a, ntiles, s, waves);
         if (smax <= 12 && (nres <= 1 || nres == kFinProj)) {

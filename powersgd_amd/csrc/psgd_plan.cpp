@@ -167,7 +167,10 @@ struct FinGeom {
 #define PSGD_FIN_RB12 1
 #endif
 int fin_rb(int R) { return R == 4 ? 1 : PSGD_FIN_RB12; }   // == FinRB<R>
-int fin_nt(int R) { return R == 4 ? 512 : 256; }  // == FinNT<R>
+#ifndef PSGD_FIN_NT4
+#define PSGD_FIN_NT4 256  // == psgd_final.cuh
+#endif
+int fin_nt(int R) { return R == 4 ? PSGD_FIN_NT4 : 256; }  // == FinNT<R>
 // scap = 0: the widest row group (T = min(threads, 4-column units rounded up to a power of
 // two), fewest segments). scap > 0: the row group with the fewest idle lanes among
 // S <= scap (ties: the narrower group — more rows per batch and, at T <= 64, a row sum
@@ -205,7 +208,7 @@ FinGeom fin_geometry(int64_t n, int64_t m, int R, int64_t fin_elems, int scap = 
 
 int fin_bucket(int s) { return s <= 2 ? 2 : s <= 3 ? 3 : s <= 5 ? 5 : s <= 12 ? 12 : 0; }
 // widest register-segment instance of the K-term final kernels per rank bucket (psgd_final.cuh)
-int fin_smax_inst(int R) { return R <= 2 ? 5 : 3; }
+int fin_smax_inst(int R) { return R <= 2 || PSGD_FIN_NT4 == 256 ? 5 : 3; }
 
 // Device-resident pointer tables (gradients, destinations) without a host synchronisation.
 // kSlots tables live in the caller's workspace; a call whose pointer set matches a slot uses
