@@ -337,3 +337,38 @@ def test_even_full_width_plans(rank, dt):
                 check(_rel(gd[i].float(), gc[i], g), tol, rank, str(dt), len(shapes), i, "res")
         for x, y in zip(runs[0], runs[1]):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_rank4_projection_wide_rows(dt):
+    """The rank-4 projection pass at 256 threads with up to 5 register segments per thread: the
+    9c-column rows of the 3x3 convolutions (4608, 2304, 1152, 576 columns: 5 segments of 256,
+    128, 64, 32 threads) and a plain 1024-column row, fp32 and bf16, one step against the
+    oracle from the same state and a bitwise rerun."""
+    shapes = [(512, 4608), (96, 2304), (2048, 1152), (64, 576), (300, 1024)]
+    psgd = PowerSGD([torch.zeros(s, device=DEV, dtype=dt) for s in shapes], Config(4, 2, 2, 0))
+    p0 = psgd._powersgd._ps_buffer.clone()
+    q0 = psgd._powersgd._qs_buffer.clone()
+    gin = [torch.from_numpy(f).to(DEV).to(dt) for f in hash_tensors(shapes, seed=97)]
+    ora = O.policy_init([torch.zeros(s) for s in shapes], 4, 2, 2, 0)
+    ora.codec.p_flat.copy_(p0.cpu())
+    ora.codec.q_flat.copy_(q0.cpu())
+    gc = [g.float().cpu() for g in gin]
+    scale = [g.clone() for g in gc]
+    oc = O.policy_step(ora, gc)
+    runs = []
+    for _ in range(2):
+        psgd._powersgd._ps_buffer.copy_(p0)
+        psgd._powersgd._qs_buffer.copy_(q0)
+        psgd.step_counter = psgd._powersgd.step_counter = 0
+        gd = [g.clone() for g in gin]
+        od = psgd.aggregate(gd)
+        torch.cuda.synchronize()
+        runs.append([o.clone() for o in od] + [g.clone() for g in gd] + [psgd._powersgd._qs_buffer.clone(),
+                                                                        psgd._powersgd._ps_buffer.clone()])
+        tol = TOL_BF16 if dt == torch.bfloat16 else TOL_STEP
+        for i, g in enumerate(scale):
+            check(_rel(od[i].float(), oc[i], g), tol, str(dt), i, "out")
+            check(_rel(gd[i].float(), gc[i], g), tol, str(dt), i, "res")
+    for x, y in zip(runs[0], runs[1]):
+        assert torch.equal(x, y)
