@@ -514,8 +514,8 @@ __global__ __launch_bounds__(FinNT<1>::value) void k_final_oe(FinalArgs a) {
 #ifndef PSGD_PROJ1_WPE
 #define PSGD_PROJ1_WPE 1
 #endif
-// Projection form: capped at 128 VGPRs (4 waves per SIMD, i.e. two 512-thread workgroups per
-// CU at rank 4; uncapped it takes 135 and drops to one workgroup per CU)
+// Projection form: rank 4 at PSGD_PROJ4_WPE waves per SIMD (2: the 256-thread, 5-segment
+// instance's 187 VGPRs; see PSGD_FIN_NT4), rank 1 at PSGD_PROJ1_WPE, rank 2 uncapped
 template <typename T, int R, int SMAX>
 __global__ __launch_bounds__(FinNT<R>::value) __attribute__((amdgpu_waves_per_eu(R == 4 ? PSGD_PROJ4_WPE : R == 1 ? PSGD_PROJ1_WPE : 1))) void k_final_proj(
     FinalArgs a) {
