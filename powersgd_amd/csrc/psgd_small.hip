@@ -827,6 +827,12 @@ struct CholNT {
 #ifndef PSGD_CHOL_U2
 #define PSGD_CHOL_U2 8
 #endif
+// panels of one load batch keep their rows in registers for the second pass (no L2 re-read):
+// rank 4 only (k_orth_chol<4> 6.48 -> 6.26 us on cfg3's P panels; rank 2 +0.3 us on cfg4's,
+// profiles/r05/orth)
+#ifndef PSGD_CHOL_RES
+#define PSGD_CHOL_RES 1
+#endif
 #ifndef PSGD_CHOL_U4
 #define PSGD_CHOL_U4 8
 #endif
@@ -854,6 +860,10 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     double g[NG];
 #pragma unroll
     for (int e = 0; e < NG; ++e) g[e] = 0.0;
+    // PSGD_CHOL_RES: a panel of one batch keeps its rows in registers for the second pass
+    constexpr bool kRes = PSGD_CHOL_RES != 0 && R == 4;
+    const bool res = kRes && k <= int64_t(kU) * NT;
+    float xr[kRes ? kU : 1][R];
     for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
         float x[kU][R];
 #pragma unroll
@@ -879,6 +889,10 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
             for (int c = 0; c < R; ++c)
 #pragma unroll
                 for (int b = c; b < R; ++b) g[e++] += double(x[q][c]) * double(x[q][b]);
+            if constexpr (kRes) {
+#pragma unroll
+                for (int c = 0; c < R; ++c) xr[q][c] = x[q][c];
+            }
         }
     }
     PSGD_STAMP(11);
@@ -934,10 +948,17 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     __syncthreads();  // every thread has read the top block before any row is overwritten
     for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
         float x[kU][R];
+        if (kRes && res) {
 #pragma unroll
-        for (int q = 0; q < kU; ++q) {
-            const int64_t i = i0 + int64_t(q) * NT;
-            ld_row<R>(st + (i < k ? i : 0) * r, r, x[q]);
+            for (int q = 0; q < kU; ++q)
+#pragma unroll
+                for (int c = 0; c < R; ++c) x[q][c] = xr[kRes ? q : 0][c];
+        } else {
+#pragma unroll
+            for (int q = 0; q < kU; ++q) {
+                const int64_t i = i0 + int64_t(q) * NT;
+                ld_row<R>(st + (i < k ? i : 0) * r, r, x[q]);
+            }
         }
 #pragma unroll
         for (int q = 0; q < kU; ++q) {
