@@ -841,7 +841,8 @@ struct CholNT {
 template <int R>
 constexpr bool kGramLds = R <= 4;
 
-template <int R, int RC>
+// KU: rows per thread per load batch (0: the PSGD_CHOL_U* default of the rank)
+template <int R, int RC, int KU = 0>
 __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUnit& u, double* redd, float* red,
                                                 float* tau, double* gpart, float* top_sh) {
     constexpr int NG = R * (R + 1) / 2;
@@ -856,7 +857,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     // rows in batches of kU per thread, all loads of a batch issued together (clamped
     // rows, masked afterwards): the panel was just written by another kernel, so each
     // batch costs one L2/MALL round trip rather than one per row
-    constexpr int kU = R <= 2 ? PSGD_CHOL_U2 : R <= 4 ? PSGD_CHOL_U4 : 4;
+    constexpr int kU = KU > 0 ? KU : R <= 2 ? PSGD_CHOL_U2 : R <= 4 ? PSGD_CHOL_U4 : 4;
     double g[NG];
 #pragma unroll
     for (int e = 0; e < NG; ++e) g[e] = 0.0;
@@ -981,7 +982,9 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
     }
 }
 
-template <int R>
+// KU > 0: load batches of KU rows per thread (the rank-4 instance for panels above one default
+// batch: 4608-row Q panels at world size > 1 stay one batch, kept in registers)
+template <int R, int KU = 0>
 __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
     constexpr int NT = CholNT<R>::value;
     __shared__ double redd[NT / 64 * (R * (R + 1) / 2)];
@@ -995,9 +998,9 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chol(OrthArgs a) {
     if (u.r == 1)  // rank-1 group of a mixed-rank plan: the reference's joint norm, not QR
         orth_joint_norm<NT>(a, u, redd);
     else if (u.r == R)
-        orth_chol_panel<R, R>(a, u, redd, red, tau, gpart, top_sh);
+        orth_chol_panel<R, R, KU>(a, u, redd, red, tau, gpart, top_sh);
     else
-        orth_chol_panel<R, 0>(a, u, redd, red, tau, gpart, top_sh);
+        orth_chol_panel<R, 0, KU>(a, u, redd, red, tau, gpart, top_sh);
     PSGD_STAMP(14);
 }
 
@@ -1381,10 +1384,22 @@ hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, i
     return hipGetLastError();
 }
 
-hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, hipStream_t s) {
+// rank 4, panels longer than one default batch (8 x 512 rows) up to 10 x 512: the 10-row
+// batch instance (W > 1 Q panels of ResNet-50: k_orth_chol<4> ~1 us faster; on the <= 4096-row
+// P panels the default batch stays faster, profiles/r05/orth)
+#ifndef PSGD_CHOL_U4L
+#define PSGD_CHOL_U4L 10
+#endif
+constexpr int kCholKU4Long = PSGD_CHOL_U4L > PSGD_CHOL_U4 ? PSGD_CHOL_U4L : PSGD_CHOL_U4 + 1;
+hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
     switch (R) {
         case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
-        case 4: k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a); break;
+        case 4:
+            if (PSGD_CHOL_U4L > PSGD_CHOL_U4 && kmax > int64_t(PSGD_CHOL_U4) * CholNT<4>::value && kmax <= int64_t(kCholKU4Long) * CholNT<4>::value)
+                k_orth_chol<4, kCholKU4Long><<<nunits, CholNT<4>::value, 0, s>>>(a);
+            else
+                k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a);
+            break;
         case 8: k_orth_chol<8><<<nunits, CholNT<8>::value, 0, s>>>(a); break;
         case 16: k_orth_chol16<<<nunits, kC16NT, 0, s>>>(a); break;
         case 32: k_orth_chol32<<<nunits, kC16NT, 0, s>>>(a); break;
@@ -1463,7 +1478,7 @@ hipError_t launch_orth(const OrthArgs& a, int nunits, int R, int64_t kmax, bool 
     if (chol && R <= 32) {
         OrthArgs b = a;
         b.flags = diag;
-        return launch_orth_chol(b, nunits, R, s);
+        return launch_orth_chol(b, nunits, R, kmax, s);
     }
     hipError_t err = hipSuccess;
     if (env_orth_wy() && launch_orth_wy(a, nunits, R, kmax, s, &err)) return err;
