@@ -862,7 +862,7 @@ __device__ __forceinline__ void orth_chol_panel(const OrthArgs& a, const OrthUni
 #pragma unroll
     for (int e = 0; e < NG; ++e) g[e] = 0.0;
     // PSGD_CHOL_RES: a panel of one batch keeps its rows in registers for the second pass
-    constexpr bool kRes = PSGD_CHOL_RES != 0 && R == 4;
+    constexpr bool kRes = PSGD_CHOL_RES != 0 && (R == 4 || KU > 0);
     const bool res = kRes && k <= int64_t(kU) * NT;
     float xr[kRes ? kU : 1][R];
     for (int64_t i0 = tid; i0 < k; i0 += int64_t(kU) * NT) {
@@ -1391,9 +1391,19 @@ hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, i
 #define PSGD_CHOL_U4L 10
 #endif
 constexpr int kCholKU4Long = PSGD_CHOL_U4L > PSGD_CHOL_U4 ? PSGD_CHOL_U4L : PSGD_CHOL_U4 + 1;
+// rank 2, panels up to 22 x 512 rows (LLaMA's 11008-row Q panels) in one register-resident batch
+#ifndef PSGD_CHOL_U2L
+#define PSGD_CHOL_U2L 22
+#endif
+constexpr int kCholKU2Long = PSGD_CHOL_U2L > PSGD_CHOL_U2 ? PSGD_CHOL_U2L : PSGD_CHOL_U2 + 1;
 hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, int64_t kmax, hipStream_t s) {
     switch (R) {
-        case 2: k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a); break;
+        case 2:
+            if (PSGD_CHOL_U2L > PSGD_CHOL_U2 && kmax > int64_t(PSGD_CHOL_U2) * CholNT<2>::value && kmax <= int64_t(kCholKU2Long) * CholNT<2>::value)
+                k_orth_chol<2, kCholKU2Long><<<nunits, CholNT<2>::value, 0, s>>>(a);
+            else
+                k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a);
+            break;
         case 4:
             if (PSGD_CHOL_U4L > PSGD_CHOL_U4 && kmax > int64_t(PSGD_CHOL_U4) * CholNT<4>::value && kmax <= int64_t(kCholKU4Long) * CholNT<4>::value)
                 k_orth_chol<4, kCholKU4Long><<<nunits, CholNT<4>::value, 0, s>>>(a);
