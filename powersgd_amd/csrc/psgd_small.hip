@@ -1391,6 +1391,11 @@ hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, i
 #define PSGD_CHOL_U4L 10
 #endif
 constexpr int kCholKU4Long = PSGD_CHOL_U4L > PSGD_CHOL_U4 ? PSGD_CHOL_U4L : PSGD_CHOL_U4 + 1;
+// rank 4, panels of at most 4 x 512 rows (ResNet-50's P panels): 4-row batches, no clamped loads
+#ifndef PSGD_CHOL_U4S
+#define PSGD_CHOL_U4S 4
+#endif
+constexpr int kCholKU4Short = PSGD_CHOL_U4S > 0 ? PSGD_CHOL_U4S : 1;
 // rank 2, panels up to 22 x 512 rows (LLaMA's 11008-row Q panels) in one register-resident batch
 #ifndef PSGD_CHOL_U2L
 #define PSGD_CHOL_U2L 22
@@ -1405,7 +1410,9 @@ hipError_t launch_orth_chol(const OrthArgs& a, int nunits, int R, int64_t kmax, 
                 k_orth_chol<2><<<nunits, CholNT<2>::value, 0, s>>>(a);
             break;
         case 4:
-            if (PSGD_CHOL_U4L > PSGD_CHOL_U4 && kmax > int64_t(PSGD_CHOL_U4) * CholNT<4>::value && kmax <= int64_t(kCholKU4Long) * CholNT<4>::value)
+            if (PSGD_CHOL_U4S > 0 && PSGD_CHOL_U4S < PSGD_CHOL_U4 && kmax <= int64_t(kCholKU4Short) * CholNT<4>::value)
+                k_orth_chol<4, kCholKU4Short><<<nunits, CholNT<4>::value, 0, s>>>(a);
+            else if (PSGD_CHOL_U4L > PSGD_CHOL_U4 && kmax > int64_t(PSGD_CHOL_U4) * CholNT<4>::value && kmax <= int64_t(kCholKU4Long) * CholNT<4>::value)
                 k_orth_chol<4, kCholKU4Long><<<nunits, CholNT<4>::value, 0, s>>>(a);
             else
                 k_orth_chol<4><<<nunits, CholNT<4>::value, 0, s>>>(a);
