@@ -1297,11 +1297,16 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol32(OrthArgs a) { orth_chol_
 // fp64 row products as k_orth_chol's second pass): the panel is read once, spread over
 // ceil(k / kChainRows) CUs instead of one. A panel the chain rejects takes the exact
 // Householder recursion in slice 0 (the other slices return).
+// rows per thread of k_orth_chain: 1 (one 512-row slice per workgroup; cfg3 0.0911-0.0912 ->
+// 0.0908 ms against 2, 4 slower: 0.0914-0.0915, profiles/r05/orth/r05ar_chain_rows.txt)
+#ifndef PSGD_CHAIN_ROWS
+#define PSGD_CHAIN_ROWS 1
+#endif
 template <int R>
 __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chain(ChainArgs a) {
     constexpr int NT = CholNT<R>::value;
     constexpr int NG = R * (R + 1) / 2;
-    constexpr int kRows = 2;  // rows per thread: kChainRows = 2 NT
+    constexpr int kRows = PSGD_CHAIN_ROWS;  // rows per thread: kChainRows = kRows NT
     __shared__ double m_sh[R * R];
     __shared__ int ok_sh;
     __shared__ float top_sh[R * R];
@@ -1375,7 +1380,7 @@ __global__ __launch_bounds__(CholNT<R>::value) void k_orth_chain(ChainArgs a) {
 
 hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, int R, hipStream_t s) {
     if (nunits == 0) return hipSuccess;
-    auto grid = [&](int nt) { return dim3(unsigned(nunits), unsigned((max_rows + 2 * nt - 1) / (2 * nt))); };
+    auto grid = [&](int nt) { return dim3(unsigned(nunits), unsigned((max_rows + PSGD_CHAIN_ROWS * nt - 1) / (PSGD_CHAIN_ROWS * nt))); };
     switch (R) {
         case 2: k_orth_chain<2><<<grid(CholNT<2>::value), CholNT<2>::value, 0, s>>>(a); break;
         case 4: k_orth_chain<4><<<grid(CholNT<4>::value), CholNT<4>::value, 0, s>>>(a); break;
