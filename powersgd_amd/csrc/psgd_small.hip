@@ -1299,12 +1299,15 @@ __global__ __launch_bounds__(kC16NT) void k_orth_chol32(OrthArgs a) { orth_chol_
 // Householder recursion in slice 0 (the other slices return).
 // rows per thread of k_orth_chain: 1 (one 512-row slice per workgroup; cfg3 0.0911-0.0912 ->
 // 0.0908 ms against 2, 4 slower: 0.0914-0.0915, profiles/r05/orth/r05ar_chain_rows.txt)
+#ifndef PSGD_CHAIN_NT
+#define PSGD_CHAIN_NT 512
+#endif
 #ifndef PSGD_CHAIN_ROWS
 #define PSGD_CHAIN_ROWS 1
 #endif
 template <int R>
-__global__ __launch_bounds__(CholNT<R>::value) void k_orth_chain(ChainArgs a) {
-    constexpr int NT = CholNT<R>::value;
+__global__ __launch_bounds__(PSGD_CHAIN_NT) void k_orth_chain(ChainArgs a) {
+    constexpr int NT = PSGD_CHAIN_NT;
     constexpr int NG = R * (R + 1) / 2;
     constexpr int kRows = PSGD_CHAIN_ROWS;  // rows per thread: kChainRows = kRows NT
     __shared__ double m_sh[R * R];
@@ -1382,8 +1385,8 @@ hipError_t launch_orth_chain(const ChainArgs& a, int nunits, int64_t max_rows, i
     if (nunits == 0) return hipSuccess;
     auto grid = [&](int nt) { return dim3(unsigned(nunits), unsigned((max_rows + PSGD_CHAIN_ROWS * nt - 1) / (PSGD_CHAIN_ROWS * nt))); };
     switch (R) {
-        case 2: k_orth_chain<2><<<grid(CholNT<2>::value), CholNT<2>::value, 0, s>>>(a); break;
-        case 4: k_orth_chain<4><<<grid(CholNT<4>::value), CholNT<4>::value, 0, s>>>(a); break;
+        case 2: k_orth_chain<2><<<grid(PSGD_CHAIN_NT), PSGD_CHAIN_NT, 0, s>>>(a); break;
+        case 4: k_orth_chain<4><<<grid(PSGD_CHAIN_NT), PSGD_CHAIN_NT, 0, s>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
