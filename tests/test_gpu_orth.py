@@ -113,3 +113,29 @@ def test_zero_and_rank_deficient_panels(rank):
             assert float((outs[i].cpu() - oc[i]).norm()) / scale <= 1e-5, (t, i)
             assert float((gd[i].cpu() - gc[i]).norm()) / scale <= 1e-5, (t, i)
         g = [r.cpu() + x for r, x in zip(gd, g)]
+
+
+@pytest.mark.parametrize("rank", [2, 4])
+@pytest.mark.parametrize("k", [2048, 2049, 4096, 4097, 5120, 5121, 11264, 11265])
+def test_panel_length_instances(rank, k):
+    """k_orth_chol picks its load-batch instance from the launch's longest panel (rank 4: 4-row
+    batches up to 2048 rows, 10-row register-resident batches for 4097-5120; rank 2: 22-row
+    batches for 4097-11264; the default batch otherwise). Panels at each side of every boundary,
+    beside short panels of the same launch, against the oracle's LAPACK state: step 0
+    orthonormalises the P panels (k rows), step 1 (I = 1, alternating) the Q panels."""
+    shapes = [(k, 16), (16, k), (64, 8), (5, 40)]
+    psgd = PowerSGD([torch.zeros(s, device=DEV) for s in shapes], Config(rank, 0.1, 1, 0))
+    ora = O.policy_init([torch.zeros(s) for s in shapes], rank, 0.1, 1, 0)
+    ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
+    ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+    for t in range(2):
+        g = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=41 + t)]
+        psgd.aggregate([x.to(DEV) for x in g])
+        O.policy_step(ora, [x.clone() for x in g])
+        torch.cuda.synchronize()
+        # 1e-5 of the buffer's largest entry: the orthonormalised factor (entries <= 1) and the
+        # other one, the raw product of that step (entries up to ~sqrt(k))
+        for name, gpu, ref in (("p", psgd._powersgd._ps_buffer, ora.codec.p_flat),
+                               ("q", psgd._powersgd._qs_buffer, ora.codec.q_flat)):
+            err = float((gpu.cpu() - ref).abs().max()) / max(1.0, float(ref.abs().max()))
+            check(err, 1e-5, "orth_panel_len_" + name, rank, k, t)
