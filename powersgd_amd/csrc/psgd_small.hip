@@ -1588,7 +1588,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
         const int e0 = red_elem(true, lane, 0);
         const gptr<const float> p = pb + (e0 < cnt ? e0 : 0);
         // batches of kB partials; a wave with at most PSGD_RED_SHORT partials issues only that
-        // many loads (no clamped repeats): k_reduce 6.2 -> 5.7 us on cfg3, 5.2 -> 4.2 on cfg5,
+        // many loads (no clamped repeats): k_reduce 6.2 -> 5.5-5.7 us on cfg3,
         // cfg3 / cfg2 steps 0.0910 / 0.0757-0.0760 -> 0.0905-0.0907 / 0.0754-0.0756 ms
         // (profiles/r05/reduce)
         auto run = [&](auto KB) {
