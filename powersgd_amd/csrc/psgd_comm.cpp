@@ -5,11 +5,15 @@
 // PSGD_RCCL_LIB_FORCE=<path> (tests only) takes precedence over all of these and is read at
 // every psgd_comm_unique_id / psgd_comm_init: each communicator keeps the function table of the
 // library it was created with, so one process can hold a real and a stand-in communicator
-// (tests/stubs/rccl_stub.hip drives psgd_aggregate_comm at world size W on one GPU).
+// (tests/stubs/rccl_stub.hip drives psgd_aggregate_comm at world size W on one GPU). The override
+// needs a second, explicit opt-in (PSGD_TESTING=1) and announces itself on stderr once per
+// library: a stray PSGD_RCCL_LIB_FORCE in a training job's environment is ignored (with a
+// warning) instead of silently replacing RCCL.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -85,16 +89,32 @@ Rccl load(const char* forced) {
     return r;
 }
 
-// The library for a new communicator: PSGD_RCCL_LIB_FORCE if set (tests), else the process's
-// RCCL. Tables live for the whole process (communicators point at them).
+// The library for a new communicator: PSGD_RCCL_LIB_FORCE if set together with PSGD_TESTING=1
+// (tests), else the process's RCCL. Tables live for the whole process (communicators point at
+// them).
 const Rccl& rccl() {
     static std::mutex mu;
     static std::map<std::string, std::unique_ptr<Rccl>> libs;
     const char* forced = std::getenv("PSGD_RCCL_LIB_FORCE");
     if (forced && !*forced) forced = nullptr;
+    const char* testing = std::getenv("PSGD_TESTING");
+    const bool opted_in = testing && std::strcmp(testing, "1") == 0;
     std::lock_guard<std::mutex> lock(mu);
+    if (forced && !opted_in) {
+        static bool warned = false;
+        if (!warned)
+            std::fprintf(stderr, "libpsgd: PSGD_RCCL_LIB_FORCE=%s ignored (test-only override; needs PSGD_TESTING=1)\n",
+                         forced);
+        warned = true;
+        forced = nullptr;
+    }
     std::unique_ptr<Rccl>& slot = libs[forced ? std::string(forced) : std::string()];
-    if (!slot) slot.reset(new Rccl(load(forced)));
+    if (!slot) {
+        if (forced)
+            std::fprintf(stderr, "libpsgd: collective library replaced by %s (PSGD_RCCL_LIB_FORCE, tests only)\n",
+                         forced);
+        slot.reset(new Rccl(load(forced)));
+    }
     return *slot;
 }
 

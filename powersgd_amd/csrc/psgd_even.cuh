@@ -399,11 +399,9 @@ struct EvenWpe {
                                           : 1;
 };
 
-// DYN: the dynamic-range instance (plan even_dyn > 1, first iteration only); the static one is
-// compiled without the range loop's state (the rank-1 instance sits at the 64-VGPR cap)
-template <typename T, int R, int K, bool DYN = false>
+template <typename T, int R, int K>
 __global__ __launch_bounds__(kEvenNT)
-__attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value - (DYN && R == 1 ? 1 : 0)))) void k_even(ProductArgs a) {
+__attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value))) void k_even(ProductArgs a) {
     // ranks above 8 always take the scalar (V = 1) layout (the plan guarantees vec == 0)
     __shared__ __attribute__((aligned(16))) float red[kEvenNW * 64 * (R <= 8 ? 4 : 1) * R];
     __shared__ float ssl[kEvenNW];
@@ -420,51 +418,33 @@ __attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value - (DYN && R == 1 ? 1 
                                uint32_t(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
     }
 #endif
-    __shared__ int next_range;
-    int rg = int(blockIdx.x);
-    const int pool = int(blockIdx.x) & (kDynPools - 1);
-    for (;;) {
-        // dynamic ranges: this workgroup's next range is claimed as the current one starts (the
-        // returning atomic is waited for only after the range's segments), from its pool's head
-        if (DYN && threadIdx.x == 0) {
-            const unsigned long long k =
-                __hip_atomic_fetch_add(a.dyn_heads + pool * 16, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                a.dyn_base;
-            next_range = a.nwg + pool + kDynPools * int(k < 0x40000000ull ? k : 0x40000000ull);
+    const int rg = int(blockIdx.x);
+    const int s0 = a.wg_seg[rg], s1 = a.wg_seg[rg + 1];
+    if (s0 >= s1) return;
+    // the next segment's descriptor and gradient pointer are loaded while this one streams
+    Seg nx = a.segs[s0];
+    const void* ng = a.grads[nx.tensor];
+    for (int si = s0; si < s1; ++si) {
+        const Seg sg = uni(nx);
+        const void* gp = uni(ng);
+        if (si + 1 < s1) {
+            nx = a.segs[si + 1];
+            ng = a.grads[nx.tensor];
         }
-        const int s0 = a.wg_seg[rg], s1 = a.wg_seg[rg + 1];
-        if (s0 < s1) {
-            // the next segment's descriptor and gradient pointer are loaded while this one streams
-            Seg nx = a.segs[s0];
-            const void* ng = a.grads[nx.tensor];
-            for (int si = s0; si < s1; ++si) {
-                const Seg sg = uni(nx);
-                const void* gp = uni(ng);
-                if (si + 1 < s1) {
-                    nx = a.segs[si + 1];
-                    ng = a.grads[nx.tensor];
-                }
-                bool done = false;
-                if constexpr (R <= 8) {
-                    if (sg.vec == 2) {
-                        even_seg_full<T, R, K>(a, sg, gp, red, ssl);
-                        done = true;
-                    } else if (sg.vec) {
-                        even_seg<T, R, K, 4>(a, sg, gp, red, ssl);
-                        done = true;
-                    }
-                }
-                if (!done) even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
-#ifdef PSGD_EVEN_STAMPS
-                if (stp && threadIdx.x == 0 && si - s0 < kEvenStamps - 2) stp[1 + si - s0] = __builtin_amdgcn_s_memrealtime();
-#endif
+        bool done = false;
+        if constexpr (R <= 8) {
+            if (sg.vec == 2) {
+                even_seg_full<T, R, K>(a, sg, gp, red, ssl);
+                done = true;
+            } else if (sg.vec) {
+                even_seg<T, R, K, 4>(a, sg, gp, red, ssl);
+                done = true;
             }
         }
-        if constexpr (!DYN) break;
-        __syncthreads();  // next_range written by thread 0 (every segment epilogue ends in one too)
-        rg = next_range;
-        __syncthreads();  // read by every thread before thread 0 writes it again
-        if (rg >= a.nranges) break;
+        if (!done) even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+#ifdef PSGD_EVEN_STAMPS
+        if (stp && threadIdx.x == 0 && si - s0 < kEvenStamps - 2) stp[1 + si - s0] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 
@@ -478,12 +458,7 @@ hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg0, hipStream_t
     const dim3 grid(nwg), block(kEvenNT);
     if constexpr (kCache) {
         switch (K) {
-            case 0:
-                if (a.dyn_heads)
-                    k_even<T, R, 0, true><<<grid, block, 0, s>>>(a);
-                else
-                    k_even<T, R, 0><<<grid, block, 0, s>>>(a);
-                break;
+            case 0: k_even<T, R, 0><<<grid, block, 0, s>>>(a); break;
             case 1: k_even<T, R, 1><<<grid, block, 0, s>>>(a); break;
             case 2:
                 if constexpr (R <= 4) k_even<T, R, 2><<<grid, block, 0, s>>>(a);

@@ -147,8 +147,6 @@ struct FlatArgs {
     int32_t world;
 };
 
-constexpr int kDynPools = 8;  // k_even dynamic ranges: one head per XCD
-
 struct ProductArgs {
     const MatDesc* mats;
     const Tile* tiles;
@@ -167,14 +165,6 @@ struct ProductArgs {
     const int32_t* wg_seg;
     int32_t nwg;
     FlatArgs flat;
-    // dynamic ranges (plan even_dyn > 1): nranges ranges wg_seg[0 .. nranges]; workgroup w takes
-    // range w first, then ranges nwg + q + kDynPools * k, k = atomicAdd(dyn_heads[q]) - dyn_base
-    // for its pool q = w mod kDynPools, until past nranges (dyn_heads null: one range each). nwg
-    // and nranges are multiples of kDynPools, so every pool's head advances by the same amount
-    // per launch and one base serves all
-    unsigned long long* dyn_heads;  // kDynPools heads, 16 words apart
-    unsigned long long dyn_base;
-    int32_t nranges;
     // diagnostic builds only (-DPSGD_EVEN_STAMPS, tools/even_stamps.py): per workgroup of k_even
     // kEvenStamps 64-bit words (s_memrealtime at entry and after each segment, the XCC / HW ids)
     unsigned long long* stamps;

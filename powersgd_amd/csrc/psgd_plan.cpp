@@ -327,7 +327,6 @@ constexpr int kCUs = 256;                // MI355X
 constexpr int kEvenWpcMax = 16;          // k_even workgroups per CU (PSGD_EVEN_WPC cap)
 constexpr int kEvenWgMax = kEvenWpcMax * kCUs;  // workgroups per launch (capacity)
 constexpr int kMaxBuckets = 8;
-constexpr int kDynStride = 16;  // uint64 words between two dynamic-range heads (own 128-B line)
 
 struct psgd_plan {
     int rank = 0, iters = 0, dtype = 0;
@@ -371,15 +370,6 @@ struct psgd_plan {
     int64_t even_segc = 4096;  // k_even cost model: elements-equivalent of one segment's fixed cost
     int64_t even_min = 16384;
     int even_order = 0;  // 0: each workgroup walks down strips; 1: row blocks across strips
-    // dynamic ranges (PSGD_EVEN_DYN = F > 1, whole-plan launches only): the plan cuts F x nwg
-    // ranges; workgroup w takes range w, then further ranges from the head of its pool (w mod
-    // kDynPools, one pool per XCD), so a workgroup that streams slowly takes fewer ranges. Every
-    // range keeps its own partial slots: the summation order is fixed whatever the assignment.
-    int even_dyn = 1;
-    int32_t even_nwg = 0;               // workgroups launched (even_dyn > 1: ranges / even_dyn)
-    int32_t dyn_take = 0;               // grabs one launch makes per pool (ranges + failing grabs)
-    uint64_t dyn_base = 0;              // every pool head's value at the next launch
-    size_t o_dyn = 0;                   // kDynPools heads, kDynStride apart (zeroed at bind)
     int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
     // odd-even pass (k_final_oe: rank 1, world size 1, I >= 3): an odd iteration followed by an
     // even one inside a step in ONE gradient pass; its partials (per K-term row block, [m]) are
@@ -612,12 +602,7 @@ struct psgd_plan {
             for (size_t i = m0; i < mi; ++i) total += mats[i].n * mats[i].m;
             int64_t nwg_launch = std::max<int64_t>(
                 1, std::min<int64_t>(int64_t(even_wpc) * kCUs, (total + even_min - 1) / std::max<int64_t>(even_min, 1)));
-            // dynamic ranges: whole-plan launches only (bucket spans keep one range per workgroup);
-            // workgroups a multiple of the pool count, so the pools advance alike
-            const int64_t F = ends.size() == 1 ? std::max(1, even_dyn) : 1;
-            if (F > 1) nwg_launch = std::max<int64_t>(kDynPools, nwg_launch / kDynPools * kDynPools);
-            const int64_t nwg = nwg_launch * F;  // ranges cut below
-            even_nwg = int32_t(nwg_launch);
+            const int64_t nwg = nwg_launch;  // ranges cut below, one per workgroup
             bucket_wg.push_back(int32_t(wg_seg.size()));
             int64_t cum = 0, w = 0;
             wg_seg.push_back(int32_t(segs.size()));
@@ -737,11 +722,6 @@ struct psgd_plan {
             wg_seg.swap(flat);
             bucket_wg.swap(bw);
         }
-        // dynamic ranges: per pool, the head advances by its ranges beyond the first nwg plus one
-        // failing grab per workgroup of the pool, every launch
-        dyn_take = 0;
-        if (even_dyn > 1 && bucket_gend.empty())
-            dyn_take = (int32_t(wg_seg.size()) - 1 - even_nwg) / kDynPools + even_nwg / kDynPools;
         // pass 2: partial slabs (per matrix, per strip, segments in row order) and ss slots
         std::vector<std::vector<int64_t>> base(mats.size());
         int64_t off = (part_odd_floats + 3) & ~int64_t(3);
@@ -1218,9 +1198,6 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", resident))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
         p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
-        // ranges per workgroup (dynamic assignment); the ranges of a launch stay within the
-        // kEvenWgMax bounds the workspace holds
-        p->even_dyn = int(std::min<int64_t>(kEvenWpcMax / p->even_wpc, std::max<int64_t>(1, env_int("PSGD_EVEN_DYN", 1))));
         // segment cost: rank 4 writes 4 floats per column per segment, so fewer, longer
         // segments pay there (cfg3 k_even 23.3-23.8 -> 22.7 us at 8192); neutral at rank 1
         // (profiles/r04/j)
@@ -1312,7 +1289,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     }
     {
         const int64_t nb = std::min<int64_t>(kMaxBuckets, int64_t(p->groups.size()));
-        const int64_t wg = std::min<int64_t>(int64_t(p->even_wpc) * kCUs, total / p->even_min + 1) * p->even_dyn;
+        const int64_t wg = std::min<int64_t>(int64_t(p->even_wpc) * kCUs, total / p->even_min + 1);
         // segments beyond one per strip: one per workgroup boundary (strip walk), up to two per
         // workgroup (row blocks across strips, ragged strips)
         const int64_t extra = 2 * nb * wg;
@@ -1349,7 +1326,6 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
     p->o_tiles_fin_kt = carve(size_t(std::max<int64_t>(p->tiles_fin_kt_cap, 1)) * sizeof(Tile));
     p->o_segs = carve(size_t(std::max<int64_t>(p->segs_cap, 1)) * sizeof(Seg));
     p->o_wg_seg = carve((size_t(kMaxBuckets) * kEvenWgMax + 1) * sizeof(int32_t));
-    p->o_dyn = carve(size_t(kDynPools) * kDynStride * sizeof(uint64_t));
     p->o_red_even = carve(size_t(std::max<int64_t>(p->red_even_cap, 1)) * sizeof(RedItem));
     p->o_red_odd = carve(size_t(std::max<int64_t>(p->red_odd_cap, 1)) * sizeof(RedItem));
     p->o_units_p = carve(p->units_p.size() * sizeof(OrthUnit));
@@ -1454,7 +1430,6 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     if (!p || !P || !Q || !workspace) return fail(PSGD_ERR_VALUE, "null argument");
     if (reinterpret_cast<uintptr_t>(workspace) % 16) return fail(PSGD_ERR_LAYOUT, "workspace must be 16-byte aligned");
     DevScope scope(device);
-    const bool fresh_ws = !p->bound || p->ws != static_cast<char*>(workspace);
     p->device = device;
     p->P = static_cast<float*>(P);  // fp64 plans: double buffers (see P64/Q64)
     p->Q = static_cast<float*>(Q);
@@ -1469,11 +1444,6 @@ int psgd_plan_bind(psgd_plan* p, int32_t device, void* P, void* Q, void* workspa
     if (int st = upload(p->dev<void>(p->o_munits_q), p->munits_q.data(), p->munits_q.size() * sizeof(OrthUnit))) return st;
     if (int st = upload(p->dev<void>(p->o_units_q), p->units_q.data(), p->units_q.size() * sizeof(OrthUnit))) return st;
     PSGD_HIP(hipMemset(p->dev<void>(p->o_ss0), 0, size_t(std::max<int64_t>(p->ss0_cap, 1)) * sizeof(float)));
-    if (fresh_ws) {  // k_even's dynamic-range heads start at 0 in a new workspace (a re-bind to
-                     // the same workspace keeps them: earlier launches may still be queued)
-        PSGD_HIP(hipMemset(p->dev<void>(p->o_dyn), 0, size_t(kDynPools) * kDynStride * sizeof(uint64_t)));
-        p->dyn_base = 0;
-    }
     if (p->f64()) {
         if (int st = upload(p->dev<void>(p->o_f64_even), p->f64_even.data(), p->f64_even.size() * sizeof(Tile))) return st;
         if (int st = upload(p->dev<void>(p->o_f64_odd), p->f64_odd.data(), p->f64_odd.size() * sizeof(Tile))) return st;
@@ -1657,21 +1627,6 @@ static int even_stamps_end(psgd_plan* p, const ProductArgs& pa, hipStream_t s) {
     return PSGD_OK;
 }
 
-// k_even launch geometry: `nranges` ranges from pa.wg_seg; with dynamic ranges (whole-plan
-// launches) fewer workgroups than ranges, each pool's head base for this launch, and the bases
-// advanced by what the launch will consume (stream order keeps the launches' grabs apart)
-static void even_geometry(psgd_plan* p, ProductArgs& pa, int32_t nranges, bool whole) {
-    pa.nranges = nranges;
-    pa.nwg = nranges;
-    pa.dyn_heads = nullptr;
-    if (p->even_dyn > 1 && whole && p->even_nwg > 0 && p->even_nwg < nranges) {
-        pa.nwg = p->even_nwg;
-        pa.dyn_heads = p->dev<unsigned long long>(p->o_dyn);
-        pa.dyn_base = p->dyn_base;
-        p->dyn_base += uint64_t(p->dyn_take);
-    }
-}
-
 static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t it, hipStream_t s,
                          bool fuse, bool write_out, const FlatArgs* fl = nullptr,
                          const psgd_plan::Span* span = nullptr) {
@@ -1804,7 +1759,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         // persistent k_even: this span's workgroups [wg[0], wg[1]) of the segmentation
         pa.segs = p->dev<Seg>(p->o_segs);
         pa.wg_seg = p->dev<int32_t>(p->o_wg_seg) + sp.wg[0];
-        even_geometry(p, pa, sp.wg[1] - sp.wg[0], span == nullptr);
+        pa.nwg = sp.wg[1] - sp.wg[0];
         // world size > 1 (no output written here): the first iteration's launch also packs the
         // uncompressed tensors, ahead of every collective
         if (fl && !write_out && it == 0) pa.flat = *fl;
@@ -2144,7 +2099,7 @@ int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, 
     if (!odd) {
         pa.segs = p->dev<Seg>(p->o_segs);
         pa.wg_seg = p->dev<int32_t>(p->o_wg_seg);
-        even_geometry(p, pa, int(p->wg_seg.size()) - 1, true);
+        pa.nwg = int(p->wg_seg.size()) - 1;
         PSGD_HIP(launch_even(p->dtype, p->rbucket, nterms, pa, pa.nwg, s));
     } else {
         if (!p->tiles_ov.empty()) {

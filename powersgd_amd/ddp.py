@@ -71,6 +71,12 @@ class PowerSGDState:
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         numel = sum(p.numel() for p in self.params)
         p0 = self.params[0]
+        # the run-table kernels (psgd_runs_*) read buckets and write the residual at ONE element
+        # size, the state's: a mixed-dtype parameter list would index them at the wrong width
+        mixed = [i for i, p in enumerate(self.params) if p.dtype != p0.dtype]
+        if mixed:
+            raise RuntimeError(f"powersgd_hook needs one gradient dtype: parameter {mixed[0]} is "
+                               f"{self.params[mixed[0]].dtype}, parameter 0 is {p0.dtype}")
         self._dev_index = _require_device(p0.device)
         self._code = _DTYPES[p0.dtype] if p0.dtype in _DTYPES else None
         if self._code is None:
@@ -106,6 +112,11 @@ class PowerSGDState:
                     raise RuntimeError("parameter reached powersgd_hook twice in one iteration")
                 idx.append(i)
             buf = bucket.buffer()
+            if buf.dtype != self.residual.dtype:
+                # DDP buckets carry the gradients' dtype; anything else (e.g. a bf16 bucket under
+                # an fp32 state) would be read and written at the wrong element size
+                raise RuntimeError(f"powersgd_hook: DDP bucket dtype {buf.dtype} differs from the state's "
+                                   f"gradient dtype {self.residual.dtype}")
             runs = self._bucket_runs(bucket.index(), buf, grads, idx)
             self._ef_add(buf, runs)
             for i in idx:

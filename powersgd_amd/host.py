@@ -30,7 +30,8 @@ the codec on the GPUs:
   zeroes ``p.grad`` every step, e.g. ``optimizer.zero_grad()``, as with the DDP hook) and adds
   them to the device residual on the GPU — the same single add autograd's accumulation into
   ``p.grad`` performs in the reference flow (README.md:39-42), so the numbers are identical; the
-  compressed inputs are left untouched instead of being overwritten with the residual.
+  compressed inputs are zeroed (consumed) instead of being overwritten with the residual, so a
+  caller that skips ``zero_grad()`` still hands only fresh gradients to the next step.
   ``residual()`` copies the device residual back on demand.
 """
 from __future__ import annotations
@@ -212,6 +213,19 @@ class HostPowerSGD:
                 self.host_out[bn["lo"]:bn["hi"]].copy_(slab, non_blocking=True)
                 if not dres:
                     self.host_grads[bn["lo"]:bn["hi"]].copy_(bn["dflat"], non_blocking=True)
+        if dres:
+            # the fresh gradients now live in the device residual: the compressed host ranges are
+            # consumed (zeroed, as the reference leaves nothing of them in its inputs but the
+            # residual), so a caller that skips zero_grad() cannot add them a second time. Each
+            # bin is zeroed on the host as soon as its H2D copy has landed, under the GPU's codec
+            # and D2H work.
+            if not direct:
+                for i, g in enumerate(gradients):
+                    if self.is_compressed_mask[i]:
+                        g.zero_()
+            for bn in self.bins:
+                bn["events"][0].synchronize()
+                self.host_grads[bn["lo"]:bn["hi"]].zero_()
         for dev, (_, _, s_out) in self.streams.items():
             s_out.synchronize()
         if not direct and not dres:

@@ -162,3 +162,26 @@ def test_run_tables_one_run_per_parameter_and_only_the_latest_layout_is_kept():
     assert st._runs[0].idx == [2, 0] and st._runs[0].offs == [0, 8] and st._runs[1].idx == [1]
     # the stub codec leaves the residual in place: two iterations of ones accumulated
     assert torch.equal(f0.value(), torch.full((16,), 2.)) and torch.equal(f1.value(), torch.full((8,), 2.))
+
+
+def test_bucket_dtype_must_match_the_state():
+    """A bucket whose dtype differs from the state's gradient dtype would be read and written at
+    the wrong element size by the native run kernels: it must raise (and fail the pending
+    futures), not launch."""
+    ps = _params()
+    st = _state(ps, _Codec())
+    f1 = powersgd_hook(st, _Bucket(ps[:2], False))
+    b = _Bucket(ps[2:], True)
+    b._buf = b._buf.to(torch.bfloat16)
+    with pytest.raises(RuntimeError, match="bucket dtype"):
+        powersgd_hook(st, b)
+    with pytest.raises(RuntimeError):
+        f1.wait()
+    assert st._nseen == 0 and st._pending == []
+
+
+def test_mixed_parameter_dtypes_are_refused():
+    from powersgd_amd import Config
+    ps = [torch.nn.Parameter(torch.zeros(4, 2)), torch.nn.Parameter(torch.zeros(4, 2, dtype=torch.bfloat16))]
+    with pytest.raises(RuntimeError, match="one gradient dtype"):
+        PowerSGDState(Config(rank=1), ps)

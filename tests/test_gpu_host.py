@@ -63,8 +63,8 @@ def test_held_outputs_are_not_overwritten():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("pin", [False, True])
-def test_device_residual_variant_equals_reference_contract(pin):
+@pytest.mark.parametrize("pin,skip_zero", [(False, False), (True, False), (True, True)])
+def test_device_residual_variant_equals_reference_contract(pin, skip_zero):
     """residual="device" (outputs-only D2H; the caller hands FRESH gradients each step and the
     residual stays on the GPU) returns bitwise the outputs of the reference contract (residual
     back in the caller's tensors, next gradient accumulated onto it), and the same residual."""
@@ -81,7 +81,8 @@ def test_device_residual_variant_equals_reference_contract(pin):
         g_ref = [r + f for r, f in zip(res, fresh)]
         if pin:
             for p, f in zip(p_dev, fresh):
-                p.grad.zero_()
+                if not skip_zero:  # skip_zero: a loop that forgets zero_grad()
+                    p.grad.zero_()
                 p.grad.add_(f)  # zero_grad + backward
             g_dev = [p.grad for p in p_dev]
         else:
@@ -90,6 +91,8 @@ def test_device_residual_variant_equals_reference_contract(pin):
         out_dev = dev.aggregate(g_dev)
         for i in range(len(SHAPES)):
             assert torch.equal(out_ref[i], out_dev[i]), (t, i)
+            # every input is consumed: compressed ones now live in the device residual
+            assert not bool(g_dev[i].any()), (t, i)
         r_dev = dev.residual()
         for i, c in enumerate(ref.is_compressed_mask):
             if c:

@@ -38,6 +38,7 @@ def _run(cfg, world, steps, port, env):
     """`steps` steps of cfg at world size `world` through the stub; returns per step the largest
     output / residual errors against W oracle workers and the stub's collective count."""
     os.environ["PSGD_RCCL_LIB_FORCE"] = STUB
+    os.environ["PSGD_TESTING"] = "1"  # the override's second opt-in (psgd_comm.cpp)
     os.environ.update(env)
     from oracle import multiworker as MW
     from oracle import powersgd_oracle as O

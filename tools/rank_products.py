@@ -65,7 +65,31 @@ def run(rank):
     print(json.dumps({"rank": rank, "ms_per_step": round(ms, 4), "GBs": round(gb, 1)}))
 
 
+# rank-k flops per element of the compressed matrices, per kernel family (x 2*r):
+#   k_even: Gt X (iteration 0, no error-feedback term)                    -> 1
+#   k_product_odd / k_odd_mfma: (G - P0 Q0t) X, error feedback on the fly -> 2
+#   k_final_proj: P = G X, then residual / output = P Xt                  -> 2
+#   k_final_odd: error feedback + product + reconstruction                 -> 3
+#   k_apply: residual and output from I factors (I = 2)                    -> 2
+FLOP_TERMS = {"psgd::k_even": 1, "psgd::k_product_odd": 2, "psgd::k_odd_mfma": 2,
+              "psgd::k_final_proj": 2, "psgd::k_final_odd": 3, "psgd::k_apply": 2}
+N_CU, N_SIMD, N_XCD = 256, 4, 8
+
+
+def _pmc(d):
+    acc = defaultdict(lambda: defaultdict(list))
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").strip()
+            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: statistics.mean(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
 def analyze(d, rank):
+    """Per rank-k kernel: median us, GB/s of the gradient, TFLOP/s against the fp32 peak, and
+    (when a PMC pass is present) MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles),
+    kernel cycles = GRBM_GUI_ACTIVE / 8 (summed over the XCDs, MI355X_MICROARCH.md DVFS note),
+    and VALU active = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (SIMDs x kernel cycles)."""
     mats = _mats(rank)
     nm = sum(n * m for n, m, _ in mats)
     nmr = sum(n * m * r for n, m, r in mats)
@@ -76,22 +100,28 @@ def analyze(d, rank):
     for r in rows:
         name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").strip()
         by[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    out = []
+    pmc = _pmc(d)
     for k, v in sorted(by.items()):
-        if not k.startswith(("psgd::k_product", "psgd::k_odd_mfma")):
+        fam = next((f for f in FLOP_TERMS if k.startswith(f)), None)
+        if fam is None:
             continue
         us = statistics.median(v)
-        # even product = iteration 0 (no error-feedback terms); odd product = iteration 1
-        even = k.startswith("psgd::k_product") and k.rstrip(">").split(",")[-1].strip() == "true"
-        nres = 0 if even else 1
-        flops = 2.0 * nmr * (1 + nres)
+        flops = 2.0 * nmr * FLOP_TERMS[fam]
         tf = flops / (us * 1e-6) / 1e12
         gbs = 4.0 * nm / (us * 1e-6) / 1e9
-        out.append({"rank": rank, "kernel": k, "launches": len(v), "median_us": round(us, 2),
-                    "GBs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 3),
-                    "TFLOPs": round(tf, 2), "fp32_peak_frac": round(tf / FP32_PEAK_TFLOPS, 4),
-                    "flop_per_byte": round(flops / (4.0 * nm), 2)})
-    for o in out:
+        o = {"rank": rank, "kernel": k, "launches": len(v), "median_us": round(us, 2),
+             "GBs_of_G": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 3),
+             "TFLOPs": round(tf, 2), "fp32_peak_frac": round(tf / FP32_PEAK_TFLOPS, 4),
+             "flop_per_byte": round(flops / (4.0 * nm), 2)}
+        c = pmc.get(k)
+        if c and c.get("GRBM_GUI_ACTIVE"):
+            cyc = c["GRBM_GUI_ACTIVE"] / N_XCD
+            simd_cyc = N_CU * N_SIMD * cyc
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+                o["mfma_busy"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cyc, 4)
+            if "SQ_ACTIVE_INST_VALU" in c:
+                o["valu_active"] = round(4.0 * c["SQ_ACTIVE_INST_VALU"] / simd_cyc, 4)
+            o["pmc_clock_GHz"] = round(cyc / (us * 1e3), 3)
         print(json.dumps(o))
 
 
