@@ -170,21 +170,30 @@ int psgd_decompress_bucket(psgd_plan* plan, void* const* grads, void* out, int64
  * rank's epoch flag in its exchange buffer and polls the peers' flags (system scope, bounded: a
  * peer that never arrives sets the status word read by psgd_ipc_status instead of hanging).
  * No host barrier and no host synchronisation per step.
- *   psgd_ipc_create   allocates this rank's exchange buffer (flags + two parities x iterations
- *                     slots, room for flat_numel uncompressed values), draws a fresh session
- *                     nonce into its header and exports handle + nonce (psgd_ipc_handle_bytes
- *                     bytes). Synchronous.
+ * Exchange buffers are regions of a per-process, per-device arena that is allocated once and
+ * never freed; every peer arena chunk is mapped once per process and never unmapped. A later
+ * session of the same size gets the same region back: no free / malloc / re-map cycle between
+ * sessions (a remapped, freed allocation can never alias a new session's buffer).
+ *   psgd_ipc_create   takes this rank's exchange region (flags + two parities x iterations
+ *                     slots, room for flat_numel uncompressed values), zeroes it, draws a fresh
+ *                     session nonce into its header and exports arena handle + region offset +
+ *                     nonce (psgd_ipc_handle_bytes bytes, the nonce last). Synchronous. Allowed
+ *                     again after psgd_ipc_close (a new session on the same plan).
  *   psgd_ipc_open     the caller all-gathers the W handles (e.g. torch.distributed) and passes
- *                     them in rank order; opens the peers' buffers and reads each peer's nonce
- *                     through the mapping: a mapping that does not reach that session's buffer
- *                     (stale) is PSGD_ERR_STATE, a list whose own entry is not this rank's handle
- *                     PSGD_ERR_VALUE. Every epoch flag carries its writer's nonce in the high
- *                     32 bits and pollers accept only the nonce they opened with.
+ *                     them in rank order; maps each peer's arena chunk (first session only) and
+ *                     reads each peer's nonce through the mapping: a mapping that does not reach
+ *                     that session's region is PSGD_ERR_STATE, a list whose own entry is not this
+ *                     rank's handle PSGD_ERR_VALUE. Every epoch flag carries its writer's nonce
+ *                     in the high 32 bits and pollers accept only the nonce they opened with.
  *   psgd_aggregate_ipc the whole step on `stream` (same arguments as psgd_aggregate_comm).
  *   psgd_ipc_status   synchronous: 1 if a wait timed out since the last call (results invalid).
- *   psgd_ipc_close    synchronous: unmap the peers. Teardown is collective: every rank calls it,
- *                     then the caller runs a cross-rank barrier before any plan is destroyed
- *                     (psgd_plan_destroy frees the exchange buffer the peers may still map). */
+ *   psgd_ipc_close    synchronous: ends the session (mappings stay with the process). Teardown
+ *                     is collective: every rank calls it, then the caller runs a cross-rank
+ *                     barrier before any rank starts a new session or destroys the plan (its
+ *                     region returns to the arena and a later session re-zeroes it).
+ *   psgd_ipc_debug    diagnostics (tests): this process's arena counters, this session's region
+ *                     address and nonce, and for peer w (open sessions) the mapped address and
+ *                     the nonce read through the mapping. */
 int psgd_ipc_handle_bytes(int64_t* bytes);
 int psgd_ipc_create(psgd_plan* plan, int64_t flat_numel, void* handle_out);
 int psgd_ipc_open(psgd_plan* plan, int32_t world_size, int32_t rank, const void* handles);
@@ -192,6 +201,17 @@ int psgd_aggregate_ipc(psgd_plan* plan, void* const* grads, void* out, int64_t s
                        void* const* unc, void* flat_out, void* stream);
 int psgd_ipc_status(psgd_plan* plan, int32_t* timed_out);
 int psgd_ipc_close(psgd_plan* plan);
+typedef struct psgd_ipc_info {
+    int64_t arena_allocs;     /* arena chunks this process allocated (hipMalloc) */
+    int64_t arena_opens;      /* peer chunks this process mapped (hipIpcOpenMemHandle) */
+    int64_t arena_reuses;     /* regions served from chunks allocated earlier */
+    int64_t arena_frees;      /* chunks freed: always 0 */
+    uint64_t own_va;          /* this session's region */
+    uint64_t peer_va;         /* peer w's region as mapped here (0 when no session is open) */
+    uint32_t own_nonce;
+    uint32_t peer_nonce_seen; /* the nonce in peer w's region header, read through the mapping */
+} psgd_ipc_info;
+int psgd_ipc_debug(psgd_plan* plan, int32_t peer, psgd_ipc_info* info);
 
 /* Whole BasicPowerSGD.aggregate step for world size 1. */
 int psgd_aggregate(psgd_plan* plan, void* const* grads, void* out, int64_t step, void* stream);

@@ -65,6 +65,7 @@ _SIGNATURES = {
     "psgd_aggregate_ipc": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp], _i32),
     "psgd_ipc_status": ([_vp, _P_i32], _i32),
     "psgd_ipc_close": ([_vp], _i32),
+    "psgd_ipc_debug": ([_vp, _i32, _vp], _i32),
     "psgd_runs_create": ([_P_i64, _P_i32, _P_i64, _P_i64, _i32, _i32, _i32, ctypes.POINTER(_vp)], _i32),
     "psgd_runs_destroy": ([_vp], _i32),
     "psgd_runs_workspace_bytes": ([_vp, _P_i64], _i32),
@@ -74,6 +75,12 @@ _SIGNATURES = {
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+
+class _IpcInfo(ctypes.Structure):  # psgd_ipc_info (include/psgd.h)
+    _fields_ = [("arena_allocs", _i64), ("arena_opens", _i64), ("arena_reuses", _i64), ("arena_frees", _i64),
+                ("own_va", ctypes.c_uint64), ("peer_va", ctypes.c_uint64), ("own_nonce", ctypes.c_uint32),
+                ("peer_nonce_seen", ctypes.c_uint32)]
 
 _lib = None
 
@@ -249,6 +256,13 @@ class Plan:
 
     def ipc_close(self) -> None:
         check(lib().psgd_ipc_close(self._h))
+
+    def ipc_debug(self, peer: int = 0) -> dict:
+        """psgd_ipc_debug: the process's exchange-arena counters, this session's region address
+        and nonce, and peer `peer`'s mapped region address and the nonce read through it."""
+        info = _IpcInfo()
+        check(lib().psgd_ipc_debug(self._h, peer, ctypes.byref(info)))
+        return {f: int(getattr(info, f)) for f, _ in _IpcInfo._fields_}
 
     def fused_final(self, step: int, aggregate: bool = True) -> int:
         """Nonzero when the last iteration of ``step`` runs fused with the final pass: 2 in the

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -313,6 +314,126 @@ struct DevScope {  // make `dev` current for the scope, restore afterwards
     }
 };
 
+// ---------------------------------------------------- process-lifetime IPC exchange arena ---
+// Exchange buffers of the one-shot all-reduce (psgd_ipc_*) are REGIONS of per-device chunks that
+// this process allocates once and never frees, and every peer chunk is mapped once per process
+// and never unmapped (round 6). A session (psgd_ipc_create .. psgd_ipc_close) takes a region,
+// zeroes its header and draws a fresh nonce; a later session of the same size gets the same
+// region back. There is no hipFree -> hipMalloc -> hipIpcOpenMemHandle cycle between two
+// sessions of one process, so a peer can never be handed a mapping of a freed buffer (the
+// round-5 r05a-new mismatch: the second same-size session after a closed one read stale sums,
+// which a cached mapping of the first session's freed allocation, whose flags still carried
+// higher epochs than the new session's, produces exactly). The nonce check at open and the
+// nonce-tagged flags stay as guards.
+struct XchgChunk {
+    int device = -1;
+    char* base = nullptr;
+    size_t bytes = 0;
+    hipIpcMemHandle_t handle{};
+};
+
+class XchgArena {
+  public:
+    static constexpr size_t kAlign = 4096;
+    static constexpr size_t kMinChunk = size_t(64) << 20;
+
+    // a region of at least `bytes` on `device`: first fit in a free range, else a new chunk
+    int acquire(int device, size_t bytes, int* chunk, size_t* off) {
+        std::lock_guard<std::mutex> lock(mu_);
+        bytes = (bytes + kAlign - 1) & ~(kAlign - 1);
+        for (size_t i = 0; i < free_.size(); ++i) {
+            Range& f = free_[i];
+            if (chunks_[size_t(f.chunk)].device != device || f.bytes < bytes) continue;
+            *chunk = f.chunk;
+            *off = f.off;
+            f.off += bytes;
+            f.bytes -= bytes;
+            if (f.bytes == 0) free_.erase(free_.begin() + long(i));
+            ++reuses_;
+            return PSGD_OK;
+        }
+        XchgChunk c;
+        c.device = device;
+        c.bytes = std::max(kMinChunk, (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1));
+        if (hipMalloc(reinterpret_cast<void**>(&c.base), c.bytes) != hipSuccess)
+            return fail(PSGD_ERR_DEVICE, "hipMalloc of the IPC exchange arena failed");
+        if (hipIpcGetMemHandle(&c.handle, c.base) != hipSuccess) {
+            (void)hipFree(c.base);  // never exported: no peer can map it
+            return fail(PSGD_ERR_DEVICE, "hipIpcGetMemHandle of the IPC exchange arena failed");
+        }
+        chunks_.push_back(c);
+        ++allocs_;
+        *chunk = int(chunks_.size()) - 1;
+        *off = 0;
+        if (c.bytes > bytes) free_.push_back(Range{*chunk, bytes, c.bytes - bytes});
+        return PSGD_OK;
+    }
+    // give a region back (its bytes stay allocated and exported; adjacent free ranges merge)
+    void release(int chunk, size_t off, size_t bytes) {
+        std::lock_guard<std::mutex> lock(mu_);
+        bytes = (bytes + kAlign - 1) & ~(kAlign - 1);
+        Range r{chunk, off, bytes};
+        for (size_t i = 0; i < free_.size();) {
+            Range& f = free_[i];
+            if (f.chunk == r.chunk && (f.off + f.bytes == r.off || r.off + r.bytes == f.off)) {
+                r.off = std::min(r.off, f.off);
+                r.bytes += f.bytes;
+                free_.erase(free_.begin() + long(i));
+                i = 0;
+            } else {
+                ++i;
+            }
+        }
+        free_.push_back(r);
+    }
+    XchgChunk chunk(int i) {
+        std::lock_guard<std::mutex> lock(mu_);
+        return chunks_[size_t(i)];
+    }
+    // the process's mapping of a peer chunk: opened at the first session that needs it, kept
+    // for the life of the process (the peer never frees the chunk either)
+    int map_peer(int device, const hipIpcMemHandle_t& h, char** base) {
+        std::lock_guard<std::mutex> lock(mu_);
+        std::string key(reinterpret_cast<const char*>(&h), sizeof(h));
+        key += std::to_string(device);
+        auto it = peers_.find(key);
+        if (it != peers_.end()) {
+            *base = it->second;
+            return PSGD_OK;
+        }
+        void* v = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&v, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(PSGD_ERR_DEVICE, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        ++opens_;
+        *base = static_cast<char*>(v);
+        peers_.emplace(key, *base);
+        return PSGD_OK;
+    }
+    void counters(int64_t* out) {
+        std::lock_guard<std::mutex> lock(mu_);
+        out[0] = allocs_;   // chunks allocated (hipMalloc) by this process
+        out[1] = opens_;    // peer chunks mapped (hipIpcOpenMemHandle) by this process
+        out[2] = reuses_;   // regions served from already-allocated chunks
+        out[3] = 0;         // chunks freed: never
+    }
+
+  private:
+    struct Range {
+        int chunk;
+        size_t off, bytes;
+    };
+    std::mutex mu_;
+    std::vector<XchgChunk> chunks_;
+    std::vector<Range> free_;
+    std::map<std::string, char*> peers_;
+    int64_t allocs_ = 0, opens_ = 0, reuses_ = 0;
+};
+
+XchgArena& xchg_arena() {
+    static XchgArena* a = new XchgArena();  // never destroyed: chunks and mappings live to exit
+    return *a;
+}
+
 }  // namespace
 
 namespace psgd {
@@ -488,7 +609,9 @@ struct psgd_plan {
     // one-shot IPC all-reduce (psgd_ipc_*, psgd_aggregate_ipc): this rank's exchange buffer
     // (hipMalloc'd so that it can be exported: flags header + 2 parities x iters slots), the
     // peers' opened mappings, the slot size (floats: factor region, then the flat region)
-    char* ipc_buf = nullptr;
+    char* ipc_buf = nullptr;      // this session's region of the process's exchange arena
+    int ipc_chunk = -1;           // the region: arena chunk, byte offset and size
+    size_t ipc_off = 0, ipc_bytes = 0;
     std::vector<void*> ipc_peer;
     int ipc_world = 0, ipc_rank = -1;
     int64_t ipc_slot = 0, ipc_flat_off = 0, ipc_flat_cap = 0;
@@ -529,9 +652,10 @@ struct psgd_plan {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
         }
-        for (size_t w = 0; w < ipc_peer.size(); ++w)
-            if (ipc_peer[w] && int(w) != ipc_rank) (void)hipIpcCloseMemHandle(ipc_peer[w]);
-        if (ipc_buf) (void)hipFree(ipc_buf);  // peers must have closed it first (psgd_ipc_close)
+        // the exchange region goes back to the process's arena (never freed, never unmapped:
+        // a peer's mapping stays valid; teardown is still collective, psgd_ipc_close + barrier,
+        // so that no peer kernel reads the region when a later session re-zeroes it)
+        if (ipc_buf) xchg_arena().release(ipc_chunk, ipc_off, ipc_bytes);
         if (xerr_host) (void)hipHostFree(xerr_host);
         if (stamp_buf) (void)hipFree(stamp_buf);
     }
@@ -1951,8 +2075,9 @@ int psgd_decompress_bucket(psgd_plan* p, void* const* grads, void* out, int64_t 
 }
 
 // ------------------------------------------------- one-shot all-reduce over IPC ---
-// an exchange handle: the HIP IPC handle of the buffer, then the buffer's session nonce
-constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t) + sizeof(uint32_t);
+// an exchange handle: the HIP IPC handle of the arena chunk, the region's byte offset in it,
+// then the session nonce (last, 4 bytes)
+constexpr size_t kHandleBytes = sizeof(hipIpcMemHandle_t) + sizeof(uint64_t) + sizeof(uint32_t);
 
 int psgd_ipc_handle_bytes(int64_t* bytes) {
     if (!bytes) return fail(PSGD_ERR_VALUE, "null argument");
@@ -1965,15 +2090,31 @@ int psgd_ipc_create(psgd_plan* p, int64_t flat_numel, void* handle_out) {
     if (!p->bound) return fail(PSGD_ERR_STATE, "plan is not bound to device memory");
     if (p->f64()) return fail(PSGD_ERR_DTYPE, "the IPC all-reduce takes fp32/bf16 plans");
     if (flat_numel < 0) return fail(PSGD_ERR_VALUE, "negative flat size");
-    if (p->ipc_buf) return fail(PSGD_ERR_STATE, "exchange buffer already created");
+    if (!p->ipc_peer.empty()) return fail(PSGD_ERR_STATE, "exchange session open (psgd_ipc_close first)");
     DevScope scope(p->device);
     auto a64 = [](int64_t x) { return (x + 63) & ~int64_t(63); };
-    p->ipc_flat_off = a64(std::max<int64_t>(p->fmax, 1));
+    const int64_t flat_off = a64(std::max<int64_t>(p->fmax, 1));
+    const int64_t slot = flat_off + a64(flat_numel);
+    const size_t bytes = size_t(kXchgHeader) + size_t(2 * p->iters * slot) * sizeof(float);
+    // a region of the process's arena: this plan's previous region when it is large enough (a
+    // re-opened session), else a new one (the old one goes back to the arena)
+    if (p->ipc_buf && p->ipc_bytes < bytes) {
+        xchg_arena().release(p->ipc_chunk, p->ipc_off, p->ipc_bytes);
+        p->ipc_buf = nullptr;
+    }
+    if (!p->ipc_buf) {
+        int chunk = -1;
+        size_t off = 0;
+        if (int st = xchg_arena().acquire(p->device, bytes, &chunk, &off)) return st;
+        p->ipc_chunk = chunk;
+        p->ipc_off = off;
+        p->ipc_bytes = bytes;
+        p->ipc_buf = xchg_arena().chunk(chunk).base + off;
+    }
+    p->ipc_flat_off = flat_off;
     p->ipc_flat_cap = flat_numel;
-    p->ipc_slot = p->ipc_flat_off + a64(flat_numel);
-    const size_t bytes = size_t(kXchgHeader) + size_t(2 * p->iters * p->ipc_slot) * sizeof(float);
-    PSGD_HIP(hipMalloc(reinterpret_cast<void**>(&p->ipc_buf), bytes));
-    PSGD_HIP(hipMemset(p->ipc_buf, 0, bytes));  // flags at epoch 0
+    p->ipc_slot = slot;
+    PSGD_HIP(hipMemset(p->ipc_buf, 0, bytes));  // flags at epoch 0, error word clear
     if (!p->xerr_host) {
         PSGD_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->xerr_host), sizeof(int32_t),
                                hipHostMallocMapped | hipHostMallocCoherent));
@@ -1992,8 +2133,12 @@ int psgd_ipc_create(psgd_plan* p, int64_t flat_numel, void* handle_out) {
     }
     PSGD_HIP(hipMemcpy(p->ipc_buf + kXchgNonceOff, &p->ipc_nonce, sizeof(uint32_t), hipMemcpyHostToDevice));
     PSGD_HIP(hipDeviceSynchronize());  // zeroed before any peer can open and poll it
-    PSGD_HIP(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), p->ipc_buf));
-    std::memcpy(static_cast<char*>(handle_out) + sizeof(hipIpcMemHandle_t), &p->ipc_nonce, sizeof(uint32_t));
+    const XchgChunk c = xchg_arena().chunk(p->ipc_chunk);
+    char* h = static_cast<char*>(handle_out);
+    const uint64_t off64 = uint64_t(p->ipc_off);
+    std::memcpy(h, &c.handle, sizeof(hipIpcMemHandle_t));
+    std::memcpy(h + sizeof(hipIpcMemHandle_t), &off64, sizeof(uint64_t));
+    std::memcpy(h + sizeof(hipIpcMemHandle_t) + sizeof(uint64_t), &p->ipc_nonce, sizeof(uint32_t));
     return PSGD_OK;
 }
 
@@ -2006,37 +2151,33 @@ int psgd_ipc_open(psgd_plan* p, int32_t world, int32_t rank, const void* handles
     const char* hb = static_cast<const char*>(handles);
     std::vector<void*> peer(size_t(world), nullptr);
     std::vector<uint32_t> nonce(size_t(world), 0);
-    auto close_open = [&](int upto) {
-        for (int v = 0; v < upto; ++v)
-            if (v != rank && peer[v]) (void)hipIpcCloseMemHandle(peer[v]);
-    };
+    const XchgChunk own = xchg_arena().chunk(p->ipc_chunk);
     for (int w = 0; w < world; ++w) {
         hipIpcMemHandle_t h;
-        std::memcpy(&h, hb + size_t(w) * kHandleBytes, sizeof(h));
-        std::memcpy(&nonce[w], hb + size_t(w) * kHandleBytes + sizeof(h), sizeof(uint32_t));
+        uint64_t off = 0;
+        const char* e = hb + size_t(w) * kHandleBytes;
+        std::memcpy(&h, e, sizeof(h));
+        std::memcpy(&off, e + sizeof(h), sizeof(uint64_t));
+        std::memcpy(&nonce[w], e + sizeof(h) + sizeof(uint64_t), sizeof(uint32_t));
         if (w == rank) {
             peer[w] = p->ipc_buf;
-            if (nonce[w] != p->ipc_nonce) {
-                close_open(w);
+            if (nonce[w] != p->ipc_nonce || off != uint64_t(p->ipc_off) ||
+                std::memcmp(&h, &own.handle, sizeof(h)) != 0)
                 return fail(PSGD_ERR_VALUE, "handle list: this rank's entry is not its own exchange handle");
-            }
             continue;
         }
-        const hipError_t e = hipIpcOpenMemHandle(&peer[w], h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-            close_open(w);
-            return fail(PSGD_ERR_DEVICE, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
-        }
-        // the mapping must reach THIS session's buffer of rank w: its header carries the nonce the
-        // handle announced (a stale mapping of an earlier, freed buffer does not)
+        // the peer's chunk, mapped once per process (no unmap / remap between sessions)
+        char* base = nullptr;
+        if (int st = xchg_arena().map_peer(p->device, h, &base)) return st;
+        peer[w] = base + off;
+        // the mapping must reach THIS session's region of rank w: its header carries the nonce the
+        // handle announced (a stale mapping, or an offset into another session's region, does not)
         uint32_t seen = 0;
         const hipError_t e2 = hipMemcpy(&seen, static_cast<char*>(peer[w]) + kXchgNonceOff, sizeof(uint32_t),
                                         hipMemcpyDeviceToHost);
-        if (e2 != hipSuccess || seen != nonce[w]) {
-            close_open(w + 1);
+        if (e2 != hipSuccess || seen != nonce[w])
             return fail(PSGD_ERR_STATE, "the mapping of rank " + std::to_string(w) +
                                             "'s exchange buffer does not reach this session's buffer (stale IPC mapping)");
-        }
     }
     p->ipc_peer = peer;
     p->ipc_world = world;
@@ -2050,13 +2191,34 @@ int psgd_ipc_close(psgd_plan* p) {
     if (p->ipc_peer.empty()) return PSGD_OK;
     DevScope scope(p->device);
     PSGD_HIP(hipDeviceSynchronize());  // no kernel of this rank still reads a peer buffer
-    for (size_t w = 0; w < p->ipc_peer.size(); ++w)
-        if (p->ipc_peer[w] && int(w) != p->ipc_rank) (void)hipIpcCloseMemHandle(p->ipc_peer[w]);
+    // the peer mappings stay in the process's arena (mapped once, never unmapped)
     p->ipc_peer.clear();
     p->ipc_world = 0;
     p->ipc_rank = -1;
     if (p->xerr_host) __atomic_store_n(p->xerr_host, 0, __ATOMIC_RELEASE);  // a fresh exchange
     PSGD_HIP(hipMemset(static_cast<char*>(p->ipc_buf) + kXchgErrOff, 0, sizeof(int32_t)));
+    return PSGD_OK;
+}
+
+int psgd_ipc_debug(psgd_plan* p, int32_t w, psgd_ipc_info* info) {
+    if (!p || !info) return fail(PSGD_ERR_VALUE, "null argument");
+    std::memset(info, 0, sizeof(*info));
+    int64_t c[4];
+    xchg_arena().counters(c);
+    info->arena_allocs = c[0];
+    info->arena_opens = c[1];
+    info->arena_reuses = c[2];
+    info->arena_frees = c[3];
+    info->own_va = uint64_t(reinterpret_cast<uintptr_t>(p->ipc_buf));
+    info->own_nonce = p->ipc_nonce;
+    if (p->ipc_peer.empty()) return PSGD_OK;
+    if (w < 0 || w >= p->ipc_world) return fail(PSGD_ERR_VALUE, "peer out of range");
+    DevScope scope(p->device);
+    info->peer_va = uint64_t(reinterpret_cast<uintptr_t>(p->ipc_peer[size_t(w)]));
+    uint32_t seen = 0;
+    PSGD_HIP(hipMemcpy(&seen, static_cast<char*>(p->ipc_peer[size_t(w)]) + kXchgNonceOff, sizeof(uint32_t),
+                       hipMemcpyDeviceToHost));
+    info->peer_nonce_seen = seen;
     return PSGD_OK;
 }
 

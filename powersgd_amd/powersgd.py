@@ -363,10 +363,11 @@ class BasicPowerSGD(Aggregator):
         return self._ipc_open and self._plan.ipc_status()
 
     def close_ipc(self, timeout: Optional[float] = None) -> None:
-        """Collective teardown of the IPC exchange: unmap the peers' buffers, then a barrier on
-        the exchange's own gloo group, so that no rank frees its exchange buffer while a peer
-        still maps it (include/psgd.h). Every rank must call it (``close()`` does), or leave it to
-        the exit hook. ``timeout`` (seconds) bounds the barrier (the exit hook uses it: a rank
+        """Collective teardown of the IPC exchange session: end it (the peer mappings stay with
+        the process's exchange arena), then a barrier on the exchange's own gloo group, so that
+        no rank re-zeroes its region for a new session (or hands it to another codec) while a
+        peer's exchange kernel may still read it (include/psgd.h). Every rank must call it
+        (``close()`` does), or leave it to the exit hook. ``timeout`` (seconds) bounds the barrier (the exit hook uses it: a rank
         that died must not hang the others at exit)."""
         if self._ipc_open:
             self._plan.ipc_close()

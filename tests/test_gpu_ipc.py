@@ -20,18 +20,39 @@ MAN = manifest()
 TOL_FREE = 1e-4
 
 
-def _worker(rank_id, world, key, initfile, skew, sessions=1):
+def _worker(rank_id, world, key, initfile, skew, sessions=1, extra_steps=0, logfile=None):
     os.environ["PSGD_COMM"] = "ipc"
     torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank_id, world_size=world)
     try:
-        for _ in range(sessions):
-            _session(rank_id, world, key, skew)
-            gc.collect()  # the codec (and its exchange buffer) is freed before the next one is made
+        for n in range(sessions):
+            _session(rank_id, world, key, skew, extra_steps, logfile, n)
+            gc.collect()  # the codec is freed (its exchange region returns to the arena) before the next
     finally:
         torch.distributed.destroy_process_group()
 
 
-def _session(rank_id, world, key, skew):
+def _log_session(psgd, rank_id, world, logfile, n):
+    """Per session and peer: the region addresses, the nonce each peer announced and the nonce
+    read through this process's mapping of it, and the process's arena counters."""
+    import json
+
+    plan = psgd._powersgd._plan
+    own = plan.ipc_debug(rank_id)
+    announced = [None] * world
+    torch.distributed.all_gather_object(announced, own["own_nonce"])
+    recs = []
+    for w in range(world):
+        d = plan.ipc_debug(w)
+        recs.append({"session": n, "rank": rank_id, "peer": w, "own_va": hex(d["own_va"]), "peer_va": hex(d["peer_va"]),
+                     "announced_nonce": announced[w], "nonce_seen": d["peer_nonce_seen"],
+                     "arena": [d["arena_allocs"], d["arena_opens"], d["arena_reuses"], d["arena_frees"]]})
+        assert d["peer_nonce_seen"] == announced[w], recs[-1]
+    with open(logfile, "a") as f:
+        for r in recs:
+            f.write(json.dumps(r) + "\n")
+
+
+def _session(rank_id, world, key, skew, extra_steps=0, logfile=None, n=0):
     from powersgd_amd import Config, PowerSGD
 
     info = MAN["multi"][key]
@@ -60,6 +81,15 @@ def _session(rank_id, world, key, skew):
             check(er, TOL_FREE, key, rank_id, t, i, "ipc-res")
         res = [g.cpu() for g in grads]
     assert psgd._powersgd._ipc_open
+    if logfile:
+        _log_session(psgd, rank_id, world, logfile, n)
+    # more steps on random gradients: the session's flags reach epochs far above the next
+    # session's first ones (the round-5 failing order: bench timing session, then a same-size
+    # parity session in the same processes)
+    gen = torch.Generator().manual_seed(100 + rank_id)
+    for _ in range(extra_steps):
+        psgd.aggregate([torch.randn(s, generator=gen).to(dev) for s in shapes])
+    torch.cuda.synchronize()
     assert not psgd._powersgd.ipc_status(), "a device-side exchange wait timed out"
     psgd._powersgd.close_ipc()
 
@@ -82,13 +112,39 @@ def test_ipc_skewed_ranks():
 
 def test_ipc_sessions_back_to_back():
     """Three codecs of the same shapes one after the other in the same processes, each freed
-    before the next is made: every session's exchange buffer is a fresh allocation of the same
-    size, its mappings are verified against the session nonce at open, and every session still
-    matches the reference goldens step by step."""
+    before the next is made, each session first matched to the reference goldens step by step and
+    then run 40 steps further (its flags end far above the next session's first epochs: the
+    round-5 r05a-new order). The exchange arena makes the sessions share ONE region per process:
+    per session and peer the test logs the region addresses, the nonce each peer announced and
+    the nonce read through this process's mapping, and asserts that each process allocated one
+    arena chunk, mapped each peer chunk once, freed nothing, and that every peer's region stays
+    at the same mapped address while the nonce seen through it is the current session's."""
+    import json
+
     key = sorted(k for k in MAN["multi"] if MAN["multi"][k]["world"] == 2)[0]
     with tempfile.TemporaryDirectory() as td:
-        torch.multiprocessing.spawn(_worker, args=(2, key, os.path.join(td, "init"), False, 3), nprocs=2,
+        log = os.path.join(td, "sessions.jsonl")
+        torch.multiprocessing.spawn(_worker, args=(2, key, os.path.join(td, "init"), False, 3, 40, log), nprocs=2,
                                     join=True)
+        recs = [json.loads(x) for x in open(log)]
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "ipc_sessions.jsonl")
+    try:
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        with open(out, "w") as f:
+            f.writelines(json.dumps(r) + "\n" for r in recs)
+    except OSError:
+        pass
+    assert len(recs) == 3 * 2 * 2
+    for rank in (0, 1):
+        mine = [r for r in recs if r["rank"] == rank]
+        for r in mine:
+            assert r["nonce_seen"] == r["announced_nonce"], r
+            assert r["arena"][0] == 1 and r["arena"][1] == 1 and r["arena"][3] == 0, r  # no free / re-map
+        peer = 1 - rank
+        vas = {r["peer_va"] for r in mine if r["peer"] == peer}
+        assert len(vas) == 1, mine  # the same mapped region every session
+        nonces = [r["announced_nonce"] for r in mine if r["peer"] == peer]
+        assert len(set(nonces)) == 3, nonces  # a fresh nonce per session
 
 
 def _nonce_worker(rank_id, initfile):

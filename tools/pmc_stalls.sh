@@ -20,6 +20,8 @@ for cfg in cfg2_resnet50_r1 cfg3_resnet50_r4; do
     timeout -s KILL 120 rocprofv3 --pmc $LDS --output-format csv -d "$out/$cfg/lds" -o lds -- python3 $B > "$out/$cfg/lds.log" 2>&1 || echo "lds pass failed ($cfg)"
   fi
   python3 tools/prof_summary.py "$out/$cfg" > "$out/$cfg/summary.txt"
+  [ -n "$KEEP_RAW" ] || rm -rf "$out/$cfg/stall" "$out/$cfg/lds"  # gpurun returns <= 64 MiB
+  echo "$cfg done"
 done
 for R in 1 4 8 16; do
   mkdir -p "$out/rank$R"
@@ -27,5 +29,7 @@ for R in 1 4 8 16; do
   timeout -s KILL 120 rocprofv3 --pmc $MFMA --output-format csv -d "$out/rank$R/pmc" -o pmc -- python3 tools/rank_products.py run $R > "$out/rank$R/pmc.log" 2>&1
   python3 tools/rank_products.py analyze "$out/rank$R" $R > "$out/rank$R/products.jsonl"
   python3 tools/prof_summary.py "$out/rank$R" > "$out/rank$R/summary.txt"
+  [ -n "$KEEP_RAW" ] || rm -rf "$out/rank$R/kt" "$out/rank$R/pmc"
+  echo "rank $R done"
 done
 echo done
