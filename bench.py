@@ -245,8 +245,10 @@ def main():
             if cfg == a.config:
                 continue
             m = measure(a, cfg, world, rank, dev, backend, "cold")
+            # every block carries its final pass's kernel roofline (events on the codec's stream,
+            # PMC traffic from profiles/pmc_traffic.json where measured) beside the step's
             keep = ("value", "ms_per_step", "per_rank_GBs", "roofline", "step_roofline")
-            out[key] = {k: m[k] for k in keep if key == "rank4" or k != "roofline"}
+            out[key] = {k: m[k] for k in keep}
             out[key]["config"] = m["config"]
             if rank == 0 and world == 1 and key == "rank4":
                 out[key]["post_backward"] = post_backward(a, cfg, dev)

@@ -28,7 +28,11 @@ class IpcHandle(ctypes.Structure):  # hipIpcMemHandle_t, passed BY VALUE to hipI
 
 
 def _hip():
-    h = ctypes.CDLL(HIP)
+    # the HIP runtime torch already loaded (its bundled ROCm); /opt/rocm's does not load beside it
+    import torch  # noqa: F401
+
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    h = ctypes.CDLL(lib if os.path.exists(lib) else HIP)
     h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     h.hipFree.argtypes = [ctypes.c_void_p]
     h.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
@@ -62,7 +66,7 @@ def _read(h, va, n):
     return sorted(set(buf))
 
 
-def worker(rank, initfile, rounds, sizes, out):
+def worker(rank, initfile, rounds, sizes, out, keep_open=False):
     import torch.distributed as dist
 
     dist.init_process_group("gloo", init_method=f"file://{initfile}", rank=rank, world_size=2)
@@ -81,7 +85,8 @@ def worker(rank, initfile, rounds, sizes, out):
                 _ok(h.hipIpcOpenMemHandle(ctypes.byref(va1), IpcHandle.from_buffer_copy(msg[0][1]), 1),
                     "open h1")
                 seen1 = _read(h, va1.value, n)
-                _ok(h.hipIpcCloseMemHandle(va1), "close h1")
+                if not keep_open:
+                    _ok(h.hipIpcCloseMemHandle(va1), "close h1")
             dist.barrier()
             if rank == 0:
                 _ok(h.hipFree(x1), "hipFree")
@@ -97,7 +102,9 @@ def worker(rank, initfile, rounds, sizes, out):
                 seen2 = _read(h, va2.value, n) if e == 0 else None
                 if e == 0:
                     _ok(h.hipIpcCloseMemHandle(va2), "close h2")
-                recs.append({"bytes": n, "round": r, "exporter_same_va": a1 == a2, "handles_equal": hh1 == hh2,
+                if keep_open and va2.value != va1.value:
+                    _ok(h.hipIpcCloseMemHandle(va1), "close h1")
+                recs.append({"keep_first_mapping_open": keep_open, "bytes": n, "round": r, "exporter_same_va": a1 == a2, "handles_equal": hh1 == hh2,
                              "handle_diff_bytes": [i for i in range(64) if hh1[i] != hh2[i]],
                              "importer_va1": hex(va1.value), "importer_va2": hex(va2.value or 0),
                              "importer_same_va": va1.value == va2.value, "open2_error": e,
@@ -119,16 +126,21 @@ def main():
 
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     sizes = [1 << 20, 3 << 20, 8 << 20, 64 << 20]
-    with tempfile.TemporaryDirectory() as td:
-        out = os.path.join(td, "recs.jsonl")
-        mp.spawn(worker, args=(os.path.join(td, "init"), rounds, sizes, out), nprocs=2, join=True)
-        recs = [json.loads(x) for x in open(out)]
-    for rec in recs:
-        print(json.dumps(rec))
-    print(json.dumps({"summary": {"rounds": len(recs), "stale": sum(r["stale"] for r in recs),
-                                  "exporter_same_va": sum(r["exporter_same_va"] for r in recs),
-                                  "handles_equal": sum(r["handles_equal"] for r in recs),
-                                  "importer_same_va": sum(r["importer_same_va"] for r in recs)}}))
+    # scenario 1: the importer closes its mapping before the owner frees (the documented
+    # teardown); scenario 2: the importer still holds the first mapping when the owner frees and
+    # re-allocates (a teardown out of order, or a second mapping of the same buffer left open)
+    for keep_open in (False, True):
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "recs.jsonl")
+            mp.spawn(worker, args=(os.path.join(td, "init"), rounds, sizes, out, keep_open), nprocs=2, join=True)
+            recs = [json.loads(x) for x in open(out)]
+        for rec in recs:
+            print(json.dumps(rec))
+        print(json.dumps({"summary": {"keep_first_mapping_open": keep_open, "rounds": len(recs),
+                                      "stale": sum(r["stale"] for r in recs),
+                                      "exporter_same_va": sum(r["exporter_same_va"] for r in recs),
+                                      "handles_equal": sum(r["handles_equal"] for r in recs),
+                                      "importer_same_va": sum(r["importer_same_va"] for r in recs)}}))
 
 
 if __name__ == "__main__":
