@@ -490,7 +490,6 @@ struct psgd_plan {
     int even_wpc = 4;
     int64_t even_segc = 4096;  // k_even cost model: elements-equivalent of one segment's fixed cost
     int64_t even_min = 16384;
-    int even_order = 0;  // 0: each workgroup walks down strips; 1: row blocks across strips
     int64_t segs_cap = 0, even_part_cap = 0, ss0_cap = 0;
     // odd-even pass (k_final_oe: rank 1, world size 1, I >= 3): an odd iteration followed by an
     // even one inside a step in ONE gradient pass; its partials (per K-term row block, [m]) are
@@ -730,7 +729,6 @@ struct psgd_plan {
             bucket_wg.push_back(int32_t(wg_seg.size()));
             int64_t cum = 0, w = 0;
             wg_seg.push_back(int32_t(segs.size()));
-            auto bound = [&](int64_t ww) { return (ww + 1) * total / nwg; };
             auto make = [&](size_t i, int s, int64_t r0, int64_t r1) {
                 const MatDesc& d = mats[i];
                 Seg sg{};
@@ -751,78 +749,52 @@ struct psgd_plan {
                 segs.push_back(sg);
                 ++nseg[i][size_t(s)];
             };
-            if (even_order == 1) {
-                // row blocks of ~total / nwg elements per strip, emitted block-major and strip-
-                // minor, each workgroup taking whole blocks: the workgroups that run side by side
-                // read the adjacent strips of the same rows (DRAM page locality), as a tile grid
-                const int64_t target = std::max<int64_t>(1, total / nwg);
-                for (size_t i = m0; i < mi; ++i) {
-                    const MatDesc& d = mats[i];
-                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+            // Cost model (round 4, the per-workgroup stamps of profiles/r04/b): a workgroup's
+            // time is its gradient loads plus a fixed cost per segment (descriptor loads, a
+            // fresh load batch, the epilogue: ~1.5-2 us, i.e. even_segc elements at one
+            // workgroup's streaming rate), and a scalar-column strip (V = 1: 256 B per wave
+            // load instead of 1 KB) costs 4x per element. Equal COST ranges instead of equal
+            // bytes: the first workgroup used to take the five narrow segments of conv1 and the
+            // first 64-row matrices and finish last (22 us against p99 19 us).
+            const int64_t segc = even_segc;
+            auto rowc = [&](const MatDesc& d, int64_t cols) { return cols * (d.vec ? 1 : 4); };
+            int64_t totw = nwg * segc;
+            for (size_t i = m0; i < mi; ++i) {
+                const MatDesc& d = mats[i];
+                const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                for (int s = 0; s < d.nstrip; ++s) totw += d.n * rowc(d, std::min<int64_t>(W, d.m - s * W)) + segc;
+            }
+            // (a dispatch-order skew, more cost to low block indices, was measured and does not
+            // help: the late blocks finish late whatever their share, profiles/r04/e)
+            auto wbound = [&](int64_t ww) { return ww + 1 >= nwg ? totw : (ww + 1) * totw / nwg; };
+            for (size_t i = m0; i < mi; ++i) {
+                const MatDesc& d = mats[i];
+                const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
+                for (int s = 0; s < d.nstrip; ++s) {
+                    const int64_t cols = std::min<int64_t>(W, d.m - s * W);
+                    const int64_t rc = rowc(d, cols);
+                    // k_even addresses a segment with 32-bit offsets: at most 2^30 bytes each
                     const int64_t es = dtype == PSGD_BF16 ? 2 : 4;
                     const int64_t seg_max = std::max<int64_t>(1, ((int64_t(1) << 30) / (d.m * es)) - 64);
-                    const int64_t h = std::min(seg_max, std::max<int64_t>(1, (target + W / 2) / W));
-                    for (int64_t r0 = 0; r0 < d.n; r0 += h) {
-                        const int64_t r1 = std::min(d.n, r0 + h);
-                        for (int s = 0; s < d.nstrip; ++s) {
-                            const int64_t cost = (r1 - r0) * std::min<int64_t>(W, d.m - s * W);
-                            if (w < nwg - 1 && segs.size() > size_t(wg_seg.back()) && 2 * cum + cost > 2 * bound(w)) {
+                    int64_t r0 = 0;
+                    while (r0 < d.n) {
+                        int64_t take = std::min(d.n - r0, seg_max);
+                        if (w < nwg - 1) {
+                            // rows to this range's end, after paying the segment's fixed cost
+                            const int64_t fit = (wbound(w) - cum - segc + rc / 2) / rc;
+                            if (fit <= 0) {
                                 ++w;
                                 wg_seg.push_back(int32_t(segs.size()));
+                                continue;
                             }
-                            make(i, s, r0, r1);
-                            cum += cost;
+                            take = std::min(take, fit);
                         }
-                    }
-                }
-            } else {
-                // Cost model (round 4, the per-workgroup stamps of profiles/r04/b): a workgroup's
-                // time is its gradient loads plus a fixed cost per segment (descriptor loads, a
-                // fresh load batch, the epilogue: ~1.5-2 us, i.e. even_segc elements at one
-                // workgroup's streaming rate), and a scalar-column strip (V = 1: 256 B per wave
-                // load instead of 1 KB) costs 4x per element. Equal COST ranges instead of equal
-                // bytes: the first workgroup used to take the five narrow segments of conv1 and the
-                // first 64-row matrices and finish last (22 us against p99 19 us).
-                const int64_t segc = even_segc;
-                auto rowc = [&](const MatDesc& d, int64_t cols) { return cols * (d.vec ? 1 : 4); };
-                int64_t totw = nwg * segc;
-                for (size_t i = m0; i < mi; ++i) {
-                    const MatDesc& d = mats[i];
-                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
-                    for (int s = 0; s < d.nstrip; ++s) totw += d.n * rowc(d, std::min<int64_t>(W, d.m - s * W)) + segc;
-                }
-                // (a dispatch-order skew, more cost to low block indices, was measured and does not
-                // help: the late blocks finish late whatever their share, profiles/r04/e)
-                auto wbound = [&](int64_t ww) { return ww + 1 >= nwg ? totw : (ww + 1) * totw / nwg; };
-                for (size_t i = m0; i < mi; ++i) {
-                    const MatDesc& d = mats[i];
-                    const int64_t W = int64_t(d.lanes) * (d.vec ? 4 : 1);
-                    for (int s = 0; s < d.nstrip; ++s) {
-                        const int64_t cols = std::min<int64_t>(W, d.m - s * W);
-                        const int64_t rc = rowc(d, cols);
-                        // k_even addresses a segment with 32-bit offsets: at most 2^30 bytes each
-                        const int64_t es = dtype == PSGD_BF16 ? 2 : 4;
-                        const int64_t seg_max = std::max<int64_t>(1, ((int64_t(1) << 30) / (d.m * es)) - 64);
-                        int64_t r0 = 0;
-                        while (r0 < d.n) {
-                            int64_t take = std::min(d.n - r0, seg_max);
-                            if (w < nwg - 1) {
-                                // rows to this range's end, after paying the segment's fixed cost
-                                const int64_t fit = (wbound(w) - cum - segc + rc / 2) / rc;
-                                if (fit <= 0) {
-                                    ++w;
-                                    wg_seg.push_back(int32_t(segs.size()));
-                                    continue;
-                                }
-                                take = std::min(take, fit);
-                            }
-                            make(i, s, r0, r0 + take);
-                            cum += segc + take * rc;
-                            r0 += take;
-                            if (w < nwg - 1 && cum >= wbound(w)) {  // this range is full
-                                ++w;
-                                wg_seg.push_back(int32_t(segs.size()));
-                            }
+                        make(i, s, r0, r0 + take);
+                        cum += segc + take * rc;
+                        r0 += take;
+                        if (w < nwg - 1 && cum >= wbound(w)) {  // this range is full
+                            ++w;
+                            wg_seg.push_back(int32_t(segs.size()));
                         }
                     }
                 }
@@ -1013,7 +985,7 @@ struct psgd_plan {
         if (fin_ok || fin_proj) {
             // segments per row up to the kernel bucket the widest groups already need
             // (at most 5: the exact-S bodies), for fewer idle lanes
-            const int scap = env_int("PSGD_FIN_GEOM", 1) ? std::min(fin_bucket(smax), 5) : 0;
+            const int scap = std::min(fin_bucket(smax), 5);
             // row blocks: the projection form's fin_elems; the K-term form's fin_elems_kt (its own
             // list only when both forms exist and the sizes differ; fin_rows_kt = fin_rows else)
             const int64_t fe = fin_proj ? fin_elems : fin_elems_kt;
@@ -1060,9 +1032,10 @@ struct psgd_plan {
                 grng_oe[2 * g] = oe_blocks;
                 grng_oe_items[2 * g] = int32_t(red_oe.size());
             }
-            // PSGD_OE_ROWS: K-term row blocks per odd-even block (fewer, larger blocks: fewer
-            // partials for the reduction, fewer workgroups streaming)
-            d.oe_rows = int32_t(std::min<int64_t>(d.n, int64_t(d.fin_rows_kt) * std::max<int64_t>(1, env_int("PSGD_OE_ROWS", 1))));
+            // one K-term row block per odd-even block (2 / 4 / 8 blocks merged: fewer partials
+            // for the reduction but a slower pass, cfg5 0.0322 / 0.0333 / 0.041 against 0.0307 ms,
+            // profiles/r05)
+            d.oe_rows = int32_t(std::min<int64_t>(d.n, int64_t(d.fin_rows_kt)));
             const int32_t nb = int32_t((d.n + d.oe_rows - 1) / d.oe_rows);
             for (int32_t b = 0; b < nb; ++b) tiles_oe.push_back(Tile{int32_t(i), 0, b, d.tensor});
             d.oe_blk0 = oe_blocks;
@@ -1321,7 +1294,6 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         resident = resident > 0 ? std::min(resident, 4) : 4;
         p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", resident))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
-        p->even_order = int(env_int("PSGD_EVEN_ORDER", 0));
         // segment cost: rank 4 writes 4 floats per column per segment, so fewer, longer
         // segments pay there (cfg3 k_even 23.3-23.8 -> 22.7 us at 8192); neutral at rank 1
         // (profiles/r04/j)
