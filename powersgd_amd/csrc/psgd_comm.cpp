@@ -141,16 +141,23 @@ int comm_allreduce(psgd_comm* c, float* buf, size_t n, float* buf2, size_t n2, h
     const Rccl& r = *c->lib;
     if (!r.error.empty()) return comm_fail(PSGD_ERR_STATE, r.error.c_str());
     if (c->poisoned) return comm_fail(PSGD_ERR_STATE, ("communicator unusable after an earlier failure: " + c->poison).c_str());
-    ncclResult_t e = r.group_start();
-    const char* what = "ncclGroupStart";
-    if (e == ncclSuccess) {
-        what = "ncclAllReduce";
+    ncclResult_t e = ncclSuccess;
+    const char* what = "ncclAllReduce";
+    if (!(n && n2)) {  // one collective: no group calls around it
         if (n) e = r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, s);
-        if (e == ncclSuccess && n2) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
-        const ncclResult_t e2 = r.group_end();
-        if (e == ncclSuccess && e2 != ncclSuccess) {
-            e = e2;
-            what = "ncclGroupEnd";
+        else if (n2) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
+    } else {
+        e = r.group_start();
+        what = "ncclGroupStart";
+        if (e == ncclSuccess) {
+            what = "ncclAllReduce";
+            e = r.all_reduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, s);
+            if (e == ncclSuccess) e = r.all_reduce(buf2, buf2, n2, ncclFloat32, ncclSum, c->comm, s);
+            const ncclResult_t e2 = r.group_end();
+            if (e == ncclSuccess && e2 != ncclSuccess) {
+                e = e2;
+                what = "ncclGroupEnd";
+            }
         }
     }
     if (e != ncclSuccess) {

@@ -110,22 +110,26 @@ def test_rccl_orchestration_world_w_vs_oracle(cfg, world):
     torch.multiprocessing.spawn(_positive, args=(_port(), cfg, world, 2), nprocs=1, join=True)
 
 
-def _negative(_, port, env, q):
-    rep = _run("cfg2_resnet50_r1", 4, 1, port, env)
+def _negative(_, port, cfg, world, env, q):
+    rep = _run(cfg, world, 1, port, env)
     q.put(max(rep[0][0], rep[0][1]))
 
 
-@pytest.mark.parametrize("env", [{"PSGD_STUB_MODE": "twice"},
-                                 {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "0"},   # even Q
-                                 {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "1"},   # odd P
-                                 {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "2"}],  # flat tail
-                         ids=["twice", "skip-q", "skip-p", "skip-flat"])
-def test_rccl_orchestration_negative_controls(env):
-    """A collective library that reduces twice or drops one of the step's three collectives must
-    make the W-worker comparison fail (the positive test above is able to fail)."""
+@pytest.mark.parametrize("cfg,world,env", [
+    ("cfg2_resnet50_r1", 4, {"PSGD_STUB_MODE": "twice"}),
+    ("cfg2_resnet50_r1", 4, {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "0"}),   # even Q
+    ("cfg2_resnet50_r1", 4, {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "1"}),   # odd P
+    ("cfg2_resnet50_r1", 4, {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "2"}),   # flat tail
+    # cfg5: four collectives per step; a lost middle one (iteration 1's P) must show too
+    ("cfg5_lstm_r1_i4", 8, {"PSGD_STUB_MODE": "skip", "PSGD_STUB_SKIP_AT": "1"}),
+    ("cfg5_lstm_r1_i4", 8, {"PSGD_STUB_MODE": "twice"})],
+    ids=["twice", "skip-q", "skip-p", "skip-flat", "cfg5-skip-p1", "cfg5-twice"])
+def test_rccl_orchestration_negative_controls(cfg, world, env):
+    """A collective library that reduces twice or drops one of the step's collectives must make
+    the W-worker comparison fail (the positive test above is able to fail)."""
     ctx = torch.multiprocessing.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_negative, args=(0, _port(), env, q))
+    p = ctx.Process(target=_negative, args=(0, _port(), cfg, world, env, q))
     p.start()
     err = q.get(timeout=300)
     p.join(timeout=60)
