@@ -273,3 +273,75 @@ def _one_rank_worker(_, initfile, cfg, steps):
 def test_ipc_one_rank_vs_oracle(cfg):
     with tempfile.TemporaryDirectory() as td:
         torch.multiprocessing.spawn(_one_rank_worker, args=(os.path.join(td, "init"), cfg, 3), nprocs=1, join=True)
+
+
+def _arena_worker(_, initfile):
+    """One process (W = 1 over the IPC exchange), several codecs of different sizes: two sessions
+    open at once, then a larger one after both closed, then a small one again. Every session is
+    checked against the CPU oracle for two steps; the process's exchange arena must serve them from
+    regions of its chunks (never freeing one) and re-use the regions the closed sessions returned."""
+    os.environ["PSGD_COMM"] = "ipc"
+    from oracle import powersgd_oracle as O
+    from powersgd_amd import Config, PowerSGD
+    from powersgd_amd.workloads import CONFIGS, hash_tensors
+
+    torch.distributed.init_process_group("gloo", init_method=f"file://{initfile}", rank=0, world_size=1)
+    try:
+        dev = torch.device("cuda:0")
+
+        def make(cfg):
+            c = CONFIGS[cfg]
+            shapes = c["shapes"]
+            psgd = PowerSGD([torch.zeros(s, device=dev) for s in shapes], Config(c["rank"], c["mcr"], c["iters"], 0))
+            ora = O.policy_init([torch.zeros(s) for s in shapes], c["rank"], c["mcr"], c["iters"], 0)
+            ora.codec.p_flat.copy_(psgd._powersgd._ps_buffer.cpu())
+            ora.codec.q_flat.copy_(psgd._powersgd._qs_buffer.cpu())
+            return psgd, ora, shapes, c
+
+        def steps(psgd, ora, shapes, c, seed):
+            for t in range(2):
+                new = [torch.from_numpy(f) for f in hash_tensors(shapes, seed=seed + t)]
+                gd = [x.to(dev) for x in new]
+                gc = [x.clone() for x in new]
+                od = psgd.aggregate(gd)
+                oc = O.policy_step(ora, gc)
+                torch.cuda.synchronize()
+                for i, x in enumerate(new):
+                    tol = (1e-6 if c["rank"] == 1 else 1e-5) if t == 0 else 1e-4
+                    s = max(float(x.norm()), 1e-30)
+                    check(float((od[i].cpu() - oc[i]).norm()) / s, tol, c["rank"], seed, t, i, "arena-out")
+                    check(float((gd[i].cpu() - gc[i]).norm()) / s, tol, c["rank"], seed, t, i, "arena-res")
+
+        def info(psgd):
+            return psgd._powersgd._plan.ipc_debug(0)
+
+        a = make("cfg5_lstm_r1_i4")
+        b = make("cfg2_resnet50_r1")
+        steps(*a, seed=900)
+        steps(*b, seed=910)  # both sessions open at once: two regions
+        ia, ib = info(a[0]), info(b[0])
+        assert ia["own_va"] != ib["own_va"] and ia["arena_frees"] == 0
+        a[0].close()
+        b[0].close()
+        va_a = ia["own_va"]
+        del a, b
+        gc.collect()
+        c3 = make("cfg3_resnet50_r4")  # larger factors: a region of its own size
+        steps(*c3, seed=920)
+        i3 = info(c3[0])
+        c3[0].close()
+        del c3
+        gc.collect()
+        a2 = make("cfg5_lstm_r1_i4")  # the small plan again: a region the arena got back
+        steps(*a2, seed=930)
+        i5 = info(a2[0])
+        assert i5["arena_frees"] == 0 and i5["arena_reuses"] >= 2, i5
+        assert i5["own_va"] == va_a or i5["own_va"] == i3["own_va"], (i5, va_a, i3)
+        a2[0].close()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_ipc_arena_regions_of_different_sizes():
+    with tempfile.TemporaryDirectory() as td:
+        torch.multiprocessing.spawn(_arena_worker, args=(os.path.join(td, "init"),), nprocs=1, join=True)
