@@ -75,16 +75,45 @@ __device__ __forceinline__ Seg uni(const Seg& s) {
     return u;
 }
 
+// The waves' column partials red[wave][strip column][R] (written and synchronised by the caller)
+// summed in wave-index order into ONE partial [strip columns][r] of the segment at sg.part
+// (r == R: one contiguous run, 16-byte stores of 4 consecutive sums). `cols` = strip width.
+template <int R>
+__device__ __forceinline__ void even_store(const ProductArgs& a, const Seg& sg, int cols, const float* red) {
+    const int tid = threadIdx.x;
+    const int r = sg.r;
+    const int64_t m = sg.m;
+    const int width = cols * R;  // floats per wave
+    gptr<float> part = gmut<float>(a.part) + sg.part;
+    const int64_t cbase = int64_t(sg.strip) * cols;
+    if (r == R && (width & 3) == 0 && cbase + cols <= m && (sg.part & 3) == 0) {
+        for (int i4 = tid * 4; i4 < width; i4 += kEvenNT * 4) {
+            v4f s = *reinterpret_cast<const v4f*>(red + i4);
+#pragma unroll
+            for (int w = 1; w < kEvenNW; ++w) s += *reinterpret_cast<const v4f*>(red + w * width + i4);
+            *(gptr<v4f>)(part + i4) = s;
+        }
+    } else {
+        for (int idx = tid; idx < width; idx += kEvenNT) {
+            float s = red[idx];
+#pragma unroll
+            for (int w = 1; w < kEvenNW; ++w) s += red[w * width + idx];
+            const int c = idx % R;
+            const int64_t jc = idx / R;
+            if (c < r && cbase + jc < m) part[jc * r + c] = s;
+        }
+    }
+    __syncthreads();  // `red` is written again by the next segment
+}
+
 // End of a segment: the rank-1 norm fold's share of sum_rows X^2 (strip-0 segments), the row
 // phases summed (DPP inside a wave, then the waves in index order through LDS) and ONE partial
-// [strip columns][r] stored at sg.part (r == R: one contiguous run, 16-byte stores).
+// [strip columns][r] stored at sg.part (even_store).
 template <int R, int V>
 __device__ __forceinline__ void even_epilogue(const ProductArgs& a, const Seg& sg, int L, float (&acc)[V][R],
                                               float* red, float* ssl) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane / L, ql = lane - sub * L;
-    const int r = sg.r;
-    const int64_t m = sg.m;
     const int64_t rb = sg.row0, re = sg.row1;
     // rank-1 iteration 0 with the norm folded: this strip-0 segment's share of the RAW
     // in-factor's sum of squares (rows in a fixed lane-strided order, then waves in order)
@@ -121,28 +150,7 @@ __device__ __forceinline__ void even_epilogue(const ProductArgs& a, const Seg& s
             a.ss0[sg.ss] = tot;
         }
     }
-    // partial of this segment: [strip column][r] at sg.part (r == R: one contiguous run, 16-byte
-    // stores of 4 consecutive sums)
-    gptr<float> part = gmut<float>(a.part) + sg.part;
-    const int64_t cbase = int64_t(sg.strip) * L * V;
-    if (r == R && (width & 3) == 0 && cbase + L * V <= m && (sg.part & 3) == 0) {
-        for (int i4 = tid * 4; i4 < width; i4 += kEvenNT * 4) {
-            v4f s = *reinterpret_cast<const v4f*>(red + i4);
-#pragma unroll
-            for (int w = 1; w < kEvenNW; ++w) s += *reinterpret_cast<const v4f*>(red + w * width + i4);
-            *(gptr<v4f>)(part + i4) = s;
-        }
-    } else {
-        for (int idx = tid; idx < width; idx += kEvenNT) {
-            float s = red[idx];
-#pragma unroll
-            for (int w = 1; w < kEvenNW; ++w) s += red[w * width + idx];
-            const int c = idx % R;
-            const int64_t jc = idx / R;
-            if (c < r && cbase + jc < m) part[jc * r + c] = s;
-        }
-    }
-    __syncthreads();  // `red` is written again by the next segment
+    even_store<R>(a, sg, L * V, red);
 }
 
 // A wave-uniform row of R factor values through the scalar data cache (s_load_dwordx1/2/4/8):
@@ -369,6 +377,91 @@ __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, co
     even_epilogue<R, V>(a, sg, L, acc, red, ssl);
 }
 
+// Ranks 9-32, first iteration (no error-feedback terms), m % 4 == 0 and 16-byte rows: the
+// column sums Q[j, c] = sum_i G[i, j] X[i, c] on the matrix cores (v_mfma_f32_16x16x4_f32,
+// exact fp32 FMA chains). Every wave spans the strip's 64 columns: lane l = (ri = l & 15,
+// cq = l >> 4) loads G[i + cq][c0 + 4 ri .. +3] (one 16-byte load, 4 rows x 256 B per wave
+// instruction; 8 bytes for bf16), and the four values are the A-operands (A[column quad ri][k =
+// row cq]) of four products whose B-operand is X[i + cq][16 cb + ri]: one accumulator per column
+// offset e and 16-rank block cb, D_e[4 cq + v][ri] = the partial of column c0 + 4 (4 cq + v) + e,
+// rank 16 cb + ri. The waves take 4-row groups in turn (kEvenU groups in flight per lane) and
+// meet in even_store. The VALU form of these ranks (one column per lane, the factor row as
+// vector loads) read G at 0.14 of HBM at rank 16.
+#ifndef PSGD_EVEN_U_MFMA
+#define PSGD_EVEN_U_MFMA 4
+#endif
+template <typename T, int R>
+__device__ __forceinline__ void even_seg_mfma(const ProductArgs& a, const Seg& sg, const void* gp, float* red) {
+    static_assert(R == 16 || R == 32, "16-rank blocks");
+    constexpr int RB = R / 16;
+    constexpr int U = PSGD_EVEN_U_MFMA;
+    constexpr uint32_t s = sizeof(T);
+    const int lane = threadIdx.x & 63, wave = uni(int32_t(threadIdx.x >> 6));
+    const int ri = lane & 15, cq = lane >> 4;
+    const int r = sg.r;
+    const int L = sg.lanes;  // strip width (V = 1 strips: one column per lane of the VALU form)
+    const int32_t m = int32_t(sg.m);
+    const int32_t c0 = sg.strip * L;
+    const int32_t col = c0 + 4 * ri;
+    const bool active = 4 * ri < L && col < m;  // m % 4 == 0: a quad is wholly in or out
+    const int32_t rb = sg.row0, re = sg.row1;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(static_cast<const T*>(gp) + int64_t(rb) * m), 0, int(uint32_t(re - rb) * uint32_t(m) * s),
+        0x00020000);
+    const uint32_t cofs = active ? uint32_t(col) * s : kOob;
+    const uint32_t rstride = uint32_t(m) * s;
+    const gptr<const float> xp = gconst<float>(a.x) + sg.poff;
+    f32x4_t acc[RB][4];
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[cb][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int32_t ngroups = (re - rb + 3) >> 2;
+    for (int32_t g = wave; g < ngroups; g += U * kEvenNW) {
+        float x[U][4];
+        float b[U][RB];
+        // every load of the batch before any is consumed; rows past the segment load 0 (range)
+#pragma unroll
+        for (int u = 0; u < U; ++u) BufIo<T>::ld4(rs, uint32_t(4 * (g + u * kEvenNW) + cq) * rstride + cofs, x[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t row = rb + 4 * (g + u * kEvenNW) + cq;
+            const int32_t xi = row < re ? row : rb;
+#pragma unroll
+            for (int cb = 0; cb < RB; ++cb) {
+                const int c = 16 * cb + ri;
+                b[u][cb] = xp[int64_t(xi) * r + (c < r ? c : 0)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t row = rb + 4 * (g + u * kEvenNW) + cq;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) keep(x[u][e]);
+#pragma unroll
+            for (int cb = 0; cb < RB; ++cb) {
+                keep(b[u][cb]);
+                const float bv = (row < re && 16 * cb + ri < r) ? b[u][cb] : 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[cb][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[u][e], bv, acc[cb][e], 0, 0, 0);
+            }
+        }
+    }
+    // red[wave][strip column][R]: column 16 cq + 4 v + e of the strip, rank 16 cb + ri
+    const int width = L * R;
+#pragma unroll
+    for (int cb = 0; cb < RB; ++cb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int cl = 16 * cq + 4 * v + e;
+                if (cl < L) red[wave * width + cl * R + 16 * cb + ri] = acc[cb][e][v];
+            }
+    __syncthreads();
+    even_store<R>(a, sg, L, red);
+}
+
 // Occupancy targets (waves per SIMD) per rank: the full-width path's registers, so that
 // every CU keeps enough 1 KB row loads in flight (PSGD_EVEN_WPE_R<rank> overrides for A/B runs)
 #ifndef PSGD_EVEN_WPE_R1
@@ -389,10 +482,15 @@ __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, co
 #ifndef PSGD_EVEN_WPE_BF16_R4
 #define PSGD_EVEN_WPE_BF16_R4 4
 #endif
+// ranks 16 / 32, first iteration (the matrix-core form and its scalar-column fallback)
+#ifndef PSGD_EVEN_WPE_MFMA
+#define PSGD_EVEN_WPE_MFMA 4
+#endif
 template <typename T, int R, int K>
 struct EvenWpe {
     static constexpr bool kBf = sizeof(T) == 2;
     static constexpr int value = K != 0 ? 1
+                                 : R >= 16 ? PSGD_EVEN_WPE_MFMA
                                  : R == 1 ? PSGD_EVEN_WPE_R1
                                  : R == 2 ? (kBf ? PSGD_EVEN_WPE_BF16_R2 : PSGD_EVEN_WPE_R2)
                                  : R == 4 ? (kBf ? PSGD_EVEN_WPE_BF16_R4 : PSGD_EVEN_WPE_R4)
@@ -432,6 +530,13 @@ __attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value))) void k_even(Produc
             ng = a.grads[nx.tensor];
         }
         bool done = false;
+        if constexpr (R >= 16 && K == 0) {
+            // 16-byte rows (m % 4 == 0 and an aligned base) take the matrix cores
+            if ((sg.m & 3) == 0 && (reinterpret_cast<uintptr_t>(gp) & (4 * sizeof(T) - 1)) == 0) {
+                even_seg_mfma<T, R>(a, sg, gp, red);
+                done = true;
+            }
+        }
         if constexpr (R <= 8) {
             if (sg.vec == 2) {
                 even_seg_full<T, R, K>(a, sg, gp, red, ssl);
@@ -468,6 +573,8 @@ hipError_t dispatch_even_r(int nres, const ProductArgs& a, int nwg0, hipStream_t
                 break;
             default: k_even<T, R, -1><<<grid, block, 0, s>>>(a); break;
         }
+    } else if (nres == 0) {  // ranks 16 / 32, first iteration: the matrix-core instance
+        k_even<T, R, 0><<<grid, block, 0, s>>>(a);
     } else {
         k_even<T, R, -1><<<grid, block, 0, s>>>(a);
     }
@@ -487,6 +594,8 @@ int even_resident(int R) {
         case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 2, 0>, kEvenNT, 0); break;
         case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 4, 0>, kEvenNT, 0); break;
         case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 8, 0>, kEvenNT, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 16, 0>, kEvenNT, 0); break;
+        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_even<T, 32, 0>, kEvenNT, 0); break;
         default: break;
     }
     return e == hipSuccess ? n : 0;

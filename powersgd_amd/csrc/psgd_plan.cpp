@@ -757,7 +757,11 @@ struct psgd_plan {
             // bytes: the first workgroup used to take the five narrow segments of conv1 and the
             // first 64-row matrices and finish last (22 us against p99 19 us).
             const int64_t segc = even_segc;
-            auto rowc = [&](const MatDesc& d, int64_t cols) { return cols * (d.vec ? 1 : 4); };
+            // (ranks 16 / 32: m % 4 == 0 strips stream 16-byte row quads on the matrix cores,
+            // even_seg_mfma, at the vector rate)
+            auto rowc = [&](const MatDesc& d, int64_t cols) {
+                return cols * ((d.vec || (rbucket >= 16 && d.m % 4 == 0)) ? 1 : 4);
+            };
             int64_t totw = nwg * segc;
             for (size_t i = m0; i < mi; ++i) {
                 const MatDesc& d = mats[i];
@@ -1288,9 +1292,7 @@ int psgd_plan_create(const int64_t* dims, const int32_t* ndims, int32_t num_tens
         // default: the first-iteration instance's resident workgroups per CU (capped at 4), so the
         // grid is one wave of resident workgroups (rank 4: 3 since the narrow-strip path fits 6
         // waves per SIMD; bf16 ranks 2 / 4: 2)
-        int resident = p->rbucket <= 8 ? (p->dtype == PSGD_F32 ? even_resident_f32(p->rbucket)
-                                                                : even_resident_bf16(p->rbucket))
-                                       : 0;
+        int resident = p->dtype == PSGD_F32 ? even_resident_f32(p->rbucket) : even_resident_bf16(p->rbucket);
         resident = resident > 0 ? std::min(resident, 4) : 4;
         p->even_wpc = int(std::min<int64_t>(kEvenWpcMax, std::max<int64_t>(1, env_int("PSGD_EVEN_WPC", resident))));
         p->even_min = std::max<int64_t>(1024, env_int("PSGD_EVEN_MIN", 16384));
