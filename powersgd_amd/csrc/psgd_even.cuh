@@ -390,11 +390,16 @@ __device__ __forceinline__ void even_seg(const ProductArgs& a, const Seg& sg, co
 #ifndef PSGD_EVEN_U_MFMA
 #define PSGD_EVEN_U_MFMA 4
 #endif
-template <typename T, int R>
+#ifndef PSGD_EVEN_U_MFMA32
+#define PSGD_EVEN_U_MFMA32 3  // rank 32 (k_even<float, 32, 0> 35.1 us; 3 waves per SIMD without
+                              // the 8 spilled VGPRs: 38.7-40.7 us, profiles/r06/wide/em2)
+#endif
+// VEC = false (m % 4 != 0 or an unaligned gradient): four element loads per lane instead.
+template <typename T, int R, bool VEC>
 __device__ __forceinline__ void even_seg_mfma(const ProductArgs& a, const Seg& sg, const void* gp, float* red) {
     static_assert(R == 16 || R == 32, "16-rank blocks");
     constexpr int RB = R / 16;
-    constexpr int U = PSGD_EVEN_U_MFMA;
+    constexpr int U = R == 32 ? PSGD_EVEN_U_MFMA32 : PSGD_EVEN_U_MFMA;
     constexpr uint32_t s = sizeof(T);
     const int lane = threadIdx.x & 63, wave = uni(int32_t(threadIdx.x >> 6));
     const int ri = lane & 15, cq = lane >> 4;
@@ -403,12 +408,15 @@ __device__ __forceinline__ void even_seg_mfma(const ProductArgs& a, const Seg& s
     const int32_t m = int32_t(sg.m);
     const int32_t c0 = sg.strip * L;
     const int32_t col = c0 + 4 * ri;
-    const bool active = 4 * ri < L && col < m;  // m % 4 == 0: a quad is wholly in or out
+    const bool active = 4 * ri < L && col < m;  // VEC (m % 4 == 0): a quad is wholly in or out
     const int32_t rb = sg.row0, re = sg.row1;
     const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<T*>(static_cast<const T*>(gp) + int64_t(rb) * m), 0, int(uint32_t(re - rb) * uint32_t(m) * s),
         0x00020000);
     const uint32_t cofs = active ? uint32_t(col) * s : kOob;
+    uint32_t eofs[4];  // !VEC: per column of the quad
+#pragma unroll
+    for (int e = 0; e < 4; ++e) eofs[e] = (4 * ri + e < L && col + e < m) ? uint32_t(col + e) * s : kOob;
     const uint32_t rstride = uint32_t(m) * s;
     const gptr<const float> xp = gconst<float>(a.x) + sg.poff;
     f32x4_t acc[RB][4];
@@ -422,7 +430,15 @@ __device__ __forceinline__ void even_seg_mfma(const ProductArgs& a, const Seg& s
         float b[U][RB];
         // every load of the batch before any is consumed; rows past the segment load 0 (range)
 #pragma unroll
-        for (int u = 0; u < U; ++u) BufIo<T>::ld4(rs, uint32_t(4 * (g + u * kEvenNW) + cq) * rstride + cofs, x[u]);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = uint32_t(4 * (g + u * kEvenNW) + cq) * rstride;
+            if constexpr (VEC) {
+                BufIo<T>::ld4(rs, ro + cofs, x[u]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[u][e] = BufIo<T>::ld1(rs, ro + eofs[e]);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t row = rb + 4 * (g + u * kEvenNW) + cq;
@@ -531,11 +547,12 @@ __attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value))) void k_even(Produc
         }
         bool done = false;
         if constexpr (R >= 16 && K == 0) {
-            // 16-byte rows (m % 4 == 0 and an aligned base) take the matrix cores
-            if ((sg.m & 3) == 0 && (reinterpret_cast<uintptr_t>(gp) & (4 * sizeof(T) - 1)) == 0) {
-                even_seg_mfma<T, R>(a, sg, gp, red);
-                done = true;
-            }
+            // the matrix cores, with 16-byte row quads when m % 4 == 0 and the base is aligned
+            if ((sg.m & 3) == 0 && (reinterpret_cast<uintptr_t>(gp) & (4 * sizeof(T) - 1)) == 0)
+                even_seg_mfma<T, R, true>(a, sg, gp, red);
+            else
+                even_seg_mfma<T, R, false>(a, sg, gp, red);
+            done = true;
         }
         if constexpr (R <= 8) {
             if (sg.vec == 2) {
@@ -546,7 +563,9 @@ __attribute__((amdgpu_waves_per_eu(EvenWpe<T, R, K>::value))) void k_even(Produc
                 done = true;
             }
         }
-        if (!done) even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+        if constexpr (!(R >= 16 && K == 0)) {
+            if (!done) even_seg<T, R, K, 1>(a, sg, gp, red, ssl);
+        }
 #ifdef PSGD_EVEN_STAMPS
         if (stp && threadIdx.x == 0 && si - s0 < kEvenStamps - 2) stp[1 + si - s0] = __builtin_amdgcn_s_memrealtime();
 #endif

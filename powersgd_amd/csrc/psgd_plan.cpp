@@ -935,7 +935,7 @@ struct psgd_plan {
             // reduce-scatter on full-width strips, lane sums on narrow ones); the MFMA kernel
             // pays for itself only for wider factors (16 output columns per instruction)
             const bool valu = use_rows && d.r <= 4;
-            d.odd_mfma = (use_mfma && !valu && d.r <= 16 && span < (int64_t(1) << 31)) ? 1 : 0;
+            d.odd_mfma = (use_mfma && !valu && d.r <= 32 && span < (int64_t(1) << 31)) ? 1 : 0;
             for (int c = 0; c < g.nchunk; ++c)
                 for (int s = 0; s < g.nstrip; ++s) {
                     tiles.push_back(Tile{int32_t(i), s, c, d.tensor});
@@ -1871,7 +1871,7 @@ static int compress_impl(psgd_plan* p, void* const* grads, int64_t step, int32_t
         }
         if (sp.om[1] > sp.om[0]) {
             pa.tiles = p->dev<Tile>(p->o_tiles_om) + sp.om[0];
-            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), it, pa, sp.om[1] - sp.om[0], s));
+            PSGD_HIP(launch_odd_mfma(p->dtype, p->rbucket, it, pa, sp.om[1] - sp.om[0], s));
         }
     }
 
@@ -2244,7 +2244,7 @@ int psgd_product(psgd_plan* p, void* const* grads, int32_t odd, const float* x, 
         }
         if (!p->tiles_om.empty()) {
             pa.tiles = p->dev<Tile>(p->o_tiles_om);
-            PSGD_HIP(launch_odd_mfma(p->dtype, std::min(p->rbucket, 16), nterms, pa, int(p->tiles_om.size()), s));
+            PSGD_HIP(launch_odd_mfma(p->dtype, p->rbucket, nterms, pa, int(p->tiles_om.size()), s));
         }
     }
     ReduceArgs ra{};

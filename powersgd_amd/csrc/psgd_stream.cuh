@@ -697,6 +697,28 @@ struct BufIo<bf16_t> {
     }
 };
 
+// Stage n factor values into LDS: ld(idx) (a global load from a clamped, always valid address)
+// for B strides of the workgroup at once, then st(idx, value). A plain element loop waits one
+// L2 round trip per element: apply_tile_mfma's rank-32 tiles 122.7 -> 107.4 us with it. (The
+// odd product's staging, behind its tile's gradient loads, measured slower batched: 84 -> 93.5
+// us at rank 16, profiles/r06/wide/em4.)
+template <int B, typename Ld, typename St>
+__device__ __forceinline__ void stage_lds(int n, Ld ld, St st) {
+    for (int base = threadIdx.x; base < n; base += B * kBlock) {
+        float v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int idx = base + u * kBlock;
+            v[u] = ld(idx < n ? idx : n - 1);
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int idx = base + u * kBlock;
+            if (idx < n) st(idx, v[u]);
+        }
+    }
+}
+
 // A wave owns row blocks rb (16 rows each: rows row0 + 16 (wave + 4 rb) + ri) of the tile
 // and works in ROUNDS of 16 slots (one 16-byte load per lane each), all issued together:
 //   WIDE   (strip > 64 columns): a round = 1 row block x 16 k-steps (the whole strip row);
@@ -724,8 +746,7 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
     const int nt = K >= 0 ? K : a.nres;
     constexpr int KC = K > 0 ? K : 1;
     constexpr int RP = 4 * RC;           // factor columns held per strip row in LDS
-    const bool cvalid = ri < r;
-    const int cx = cvalid ? ri : 0;
+    constexpr int RB = RP > 16 ? 2 : 1;  // 16-column blocks of the product (rank 32: two)
     const int nks = (sw + 15) >> 4;      // 16-column k-steps of the strip
     const int nrb = int((row_end - row0 - wave * 16 + kWaves * 16 - 1) / (kWaves * 16));  // >= 0
 
@@ -766,9 +787,11 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
     };
 
     auto process = [&](int rb0) {
-        f32x4_t acc[QN];
+        f32x4_t acc[QN][RB];
 #pragma unroll
-        for (int q = 0; q < QN; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < QN; ++q)
+#pragma unroll
+            for (int ob = 0; ob < RB; ++ob) acc[q][ob] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         if constexpr (K > 0) {
 #pragma unroll
             for (int q = 0; q < QN; ++q) {
@@ -825,24 +848,32 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
                     }
                 }
                 // xt rows are zero-padded to a multiple of 4 columns: one aligned 16-byte read
-                const v4f bx4 = *reinterpret_cast<const v4f*>(xt + cx * kOddXT + (jj < sw ? jj : 0));
-                const bool okx = cvalid && jj < sw;
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][0], okx ? bx4.x : 0.f, acc[q], 0, 0, 0);
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][1], okx ? bx4.y : 0.f, acc[q], 0, 0, 0);
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][2], okx ? bx4.z : 0.f, acc[q], 0, 0, 0);
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][3], okx ? bx4.w : 0.f, acc[q], 0, 0, 0);
+#pragma unroll
+                for (int ob = 0; ob < RB; ++ob) {
+                    const int c = 16 * ob + ri;
+                    const v4f bx4 = *reinterpret_cast<const v4f*>(xt + (c < r ? c : 0) * kOddXT + (jj < sw ? jj : 0));
+                    const bool okx = c < r && jj < sw;
+                    acc[q][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][0], okx ? bx4.x : 0.f, acc[q][ob], 0, 0, 0);
+                    acc[q][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][1], okx ? bx4.y : 0.f, acc[q][ob], 0, 0, 0);
+                    acc[q][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][2], okx ? bx4.z : 0.f, acc[q][ob], 0, 0, 0);
+                    acc[q][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sl][3], okx ? bx4.w : 0.f, acc[q][ob], 0, 0, 0);
+                }
             }
         }
-        // acc[q][e] = partial P[i0 + 4 cq + e][c = ri] of row block rb0 + q
-        if (cvalid) {
-            gptr<float> part = gmut<float>(a.part) + d.part_odd + int64_t(t.strip) * n * r;
+        // acc[q][ob][e] = partial P[i0 + 4 cq + e][c = 16 ob + ri] of row block rb0 + q
+        gptr<float> part = gmut<float>(a.part) + d.part_odd + int64_t(t.strip) * n * r;
 #pragma unroll
-            for (int q = 0; q < QN; ++q) {
-                const int64_t i0 = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16);
+        for (int ob = 0; ob < RB; ++ob) {
+            const int c = 16 * ob + ri;
+            if (c < r) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t ii = i0 + 4 * cq + e;
-                    if (ii < row_end) part[ii * r + ri] = acc[q][e];
+                for (int q = 0; q < QN; ++q) {
+                    const int64_t i0 = row0 + wave * 16 + int64_t(rb0 + q) * (kWaves * 16);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t ii = i0 + 4 * cq + e;
+                        if (ii < row_end) part[ii * r + c] = acc[q][ob][e];
+                    }
                 }
             }
         }
@@ -920,6 +951,8 @@ hipError_t dispatch_odd_mfma(int R, int nres, const ProductArgs& a, int ntiles, 
         PSGD_O(2);
     else if (R <= 16)
         PSGD_O(4);
+    else if (R <= 32)
+        PSGD_O(8);
     else
         return hipErrorInvalidValue;
 #undef PSGD_O
@@ -1042,6 +1075,138 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const MatDesc& d,
     }
 }
 
+// Ranks 16 / 32: the reconstruction T = sum_k P_k Q_k^T of a tile on the matrix cores
+// (v_mfma_f32_16x16x4_f32), the residual G - T and the output T (world size 1) or
+// alpha * sum_k Pbar_k Qbar_k^T (world size > 1) streamed as the VALU form does. A wave takes
+// 16-row blocks of the tile's 64-column strip; lane l = (ri = l & 15, cq = l >> 4) holds rows
+// b0 + 4 cq + v (v = 0..3) x columns c0 + 4 ri .. +3 of the block: one 16-byte gradient load,
+// residual store and output store per row (4 rows x 256 B per wave instruction), which is
+// exactly the accumulator layout of four products D_e (column offset e) with A[i][k] =
+// P_k[b0 + i][rank(k)] and B[k][n] = Q_k[c0 + 4 n + e][rank(k)]. Lane row cq owns ranks
+// cq * R/4 .. +R/4 (contiguous: one or two 16-byte LDS reads per product set). The strip's factor
+// columns (every term, both sets) are staged in LDS once per tile. The VALU form of these ranks
+// (one column per lane, r FMAs and r factor loads per element) ran at 0.08 of HBM at rank 16 and
+// 0.013 at rank 32 (profiles/r06/wide/em1).
+constexpr int kApplyMfmaSets = 4;  // staged (term, set) panels: nterms x (1 shared, 2 split) <= 4
+template <int R>
+struct ApplyMfmaLds {
+    static constexpr int RP = R + 4;  // padded LDS row (floats)
+    static constexpr int floats = kApplyMfmaSets * 64 * RP;
+};
+
+template <typename T, int R, bool SHARED, bool ONT>
+__device__ __forceinline__ void apply_tile_mfma(const ApplyArgs& a, const MatDesc& d, const Tile& t, float* qs) {
+    constexpr int KQ = R / 4;
+    constexpr int RP = ApplyMfmaLds<R>::RP;
+    constexpr int NS = SHARED ? 1 : 2;
+    constexpr uint32_t s = sizeof(T);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int ri = lane & 15, cq = lane >> 4;
+    const int r = d.r;
+    const int nt = a.nterms;
+    const int32_t m = int32_t(d.m);
+    const int L = d.lanes;
+    const int32_t cb = t.strip * L;  // V = 1 strips of L <= 64 columns
+    const int32_t col = cb + 4 * ri;
+    const bool active = 4 * ri < L && col < m;  // m % 4 == 0: a quad is wholly in or out
+    const int64_t row_begin = int64_t(t.chunk) * d.chunk_rows;
+    const int64_t row_end = d.n < row_begin + d.chunk_rows ? d.n : row_begin + d.chunk_rows;
+    // stage qs[set * nt + k][j][c] = Q_k[cb + j][c] of the set (0 past the strip or the rank)
+    auto qidx = [&](int idx, int& c, int& j, int& sk) {
+        c = idx % R;
+        j = (idx / R) % 64;
+        sk = idx / (64 * R);
+    };
+    stage_lds<8>(
+        NS * nt * 64 * R,
+        [&](int idx) {
+            int c, j, sk;
+            qidx(idx, c, j, sk);
+            const int set = sk / nt, k = sk - set * nt;
+            const float* q = set == 0 ? a.res.q[k] : a.apx.q[k];
+            const bool ok = c < r && cb + j < m && j < L;
+            const float v = gconst<float>(q)[d.qoff + (ok ? int64_t(cb + j) * r + c : 0)];
+            return ok ? v : 0.f;
+        },
+        [&](int idx, float v) {
+            int c, j, sk;
+            qidx(idx, c, j, sk);
+            qs[(sk * 64 + j) * RP + c] = v;
+        });
+    __syncthreads();
+    T* const Gp = static_cast<T*>(a.grads[t.tensor]);
+    T* const Dp = static_cast<T*>(a.rdst ? a.rdst[d.tensor] : a.grads[t.tensor]);
+    T* const Op = a.odst ? static_cast<T*>(a.odst[d.tensor]) : static_cast<T*>(a.out) + d.out_off;
+    const uint32_t tb = uint32_t((row_end - row_begin) * int64_t(m) * int64_t(s));
+    const rsrc_t rG = make_rsrc(Gp + row_begin * m, tb);
+    const rsrc_t rD = make_rsrc(Dp + row_begin * m, tb);
+    const rsrc_t rO = make_rsrc(Op + row_begin * m, tb);
+    const uint32_t cofs = active ? uint32_t(col) * s : kOob;
+    const uint32_t rstride = uint32_t(m) * s;
+    const bool pvec = r == R && (d.poff & 3) == 0;
+    const float alpha = a.alpha;
+    for (int64_t b0 = row_begin + 16 * wave; b0 < row_end; b0 += 16 * kWaves) {
+        const uint32_t rb = uint32_t(b0 - row_begin + 4 * cq);
+        float x[4][4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) BufIo<T>::ld4(rG, (rb + v) * rstride + cofs, x[v]);
+        const int64_t pi = b0 + ri < row_end ? b0 + ri : row_begin;  // A-operand row (clamped)
+        f32x4_t tacc[NS][4];
+#pragma unroll
+        for (int st = 0; st < NS; ++st)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) tacc[st][e] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int st = 0; st < NS; ++st) {
+            for (int k = 0; k < nt; ++k) {
+                const gptr<const float> P = gconst<float>(st == 0 ? a.res.p[k] : a.apx.p[k]) + d.poff + pi * r;
+                float pa[KQ];
+                if (pvec) {
+#pragma unroll
+                    for (int j = 0; j < KQ; j += 4) {
+                        const v4f w = *(gptr<const v4f>)(P + cq * KQ + j);
+                        pa[j] = w.x; pa[j + 1] = w.y; pa[j + 2] = w.z; pa[j + 3] = w.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < KQ; ++j) {
+                        const int c = cq * KQ + j;
+                        pa[j] = P[c < r ? c : 0];
+                    }
+#pragma unroll
+                    for (int j = 0; j < KQ; ++j) {
+                        keep(pa[j]);
+                        pa[j] = cq * KQ + j < r ? pa[j] : 0.f;
+                    }
+                }
+                const float* qk = qs + ((st * nt + k) * 64 + 4 * ri) * RP + cq * KQ;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < KQ; j += 4) {
+                        const v4f bq = *reinterpret_cast<const v4f*>(qk + e * RP + j);
+                        tacc[st][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j], bq.x, tacc[st][e], 0, 0, 0);
+                        tacc[st][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j + 1], bq.y, tacc[st][e], 0, 0, 0);
+                        tacc[st][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j + 2], bq.z, tacc[st][e], 0, 0, 0);
+                        tacc[st][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j + 3], bq.w, tacc[st][e], 0, 0, 0);
+                    }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            float xo[4], oo[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                xo[e] = x[v][e] - tacc[0][e][v];  // reference :195-202
+                oo[e] = SHARED ? tacc[0][e][v] : alpha * tacc[NS - 1][e][v];  // :211-219
+            }
+            const uint32_t off = (rb + v) * rstride + cofs;
+            st_vec<T>(rD, off, xo);
+            st_vec<T, ONT ? kStAuxOutNt : PSGD_ST_AUX>(rO, off, oo);
+        }
+    }
+    __syncthreads();  // qs is staged again by the next tile of this workgroup (none today)
+}
+
 // ONT: the output stores nt only (world size 1, plans above PSGD_OUT_NT_MB: the averaged
 // gradient the optimizer reads next does not sit dirty in the Infinity Cache ahead of the next
 // step's cold reads); a compile-time instance, so the store form costs no registers
@@ -1059,6 +1224,18 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a) {
     if constexpr (R <= 8) {
         if (d.vec) {
             apply_tile<T, R, NI, SHARED, 4, ONT>(a, d, t);
+            return;
+        }
+    }
+    if constexpr (R >= 16) {
+        __shared__ __attribute__((aligned(16))) float qs[ApplyMfmaLds<R>::floats];
+        constexpr int NS = SHARED ? 1 : 2;
+        const uintptr_t rows = reinterpret_cast<uintptr_t>(a.grads[t.tensor]) |
+                               reinterpret_cast<uintptr_t>(a.rdst ? a.rdst[d.tensor] : a.grads[t.tensor]) |
+                               reinterpret_cast<uintptr_t>(a.odst ? static_cast<T*>(a.odst[d.tensor])
+                                                                  : static_cast<T*>(a.out) + d.out_off);
+        if ((d.m & 3) == 0 && (rows & (4 * sizeof(T) - 1)) == 0 && a.nterms * NS <= kApplyMfmaSets) {
+            apply_tile_mfma<T, R, SHARED, ONT>(a, d, t, qs);
             return;
         }
     }
@@ -1101,10 +1278,10 @@ hipError_t dispatch_odd(int R, int nres, const ProductArgs& a, int ntiles, hipSt
 template <typename T, int R>
 hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int ntiles, hipStream_t s) {
     const dim3 grid(ntiles + a.flat.nitems), block(kBlock);
-    // register-cached factor terms: up to 4 at ranks <= 8, up to 2 at rank 16 (I <= 2);
-    // wider ranks load factor rows per element
-    constexpr bool kCache = R <= 16;
-    constexpr int kMaxNI = R <= 8 ? 4 : 2;
+    // register-cached factor terms: up to 4 at ranks <= 8; ranks 16 / 32 take the matrix-core
+    // tiles (apply_tile_mfma, any term count), whose fallback loads factor rows per element
+    constexpr bool kCache = R <= 8;
+    constexpr int kMaxNI = 4;
     // world size > 1 (two term sets: local and all-reduced) caches fewer: the 4-term rank-4
     // and rank-8 instances spilled VGPRs to scratch (tools/regs.py), the per-use loads do not
     const int maxni = shared ? kMaxNI : (R <= 2 ? 4 : R == 4 ? 3 : 2);
@@ -1118,18 +1295,12 @@ hipError_t dispatch_apply_r(int nterms, bool shared, const ApplyArgs& a, int nti
         else                                                                             \
             timed_launch(&k_apply<T, R, NN, false>, grid, block, s, a);                  \
     } while (0)
-    if constexpr (kCache && kMaxNI == 4) {
+    if constexpr (kCache) {
         switch (NI) {
             case 1: PSGD_A(1); break;
             case 2: PSGD_A(2); break;
             case 3: PSGD_A(3); break;
             case 4: PSGD_A(4); break;
-            default: PSGD_A(-1); break;
-        }
-    } else if constexpr (kCache) {
-        switch (NI) {
-            case 1: PSGD_A(1); break;
-            case 2: PSGD_A(2); break;
             default: PSGD_A(-1); break;
         }
     } else {

@@ -24,6 +24,18 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STUB = os.path.join(REPO, "tests", "stubs", "librccl_stub.so")
 
 
+# ranks 16 / 32 (the matrix-core even product and apply tiles, world size > 1: the output from
+# the all-reduced factors): ragged strips, a narrow matrix, an m % 4 != 0 matrix, a flat tail
+WIDE_SHAPES = [(300, 200), (64, 1000), (1000, 64), (96, 40), (333, 148), (200, 150), (40,), (130, 16, 3, 3)]
+WIDE = {"wide16": {"shapes": WIDE_SHAPES, "rank": 16, "mcr": 0.1, "iters": 2, "dtype": "f32"},
+        "wide32": {"shapes": WIDE_SHAPES, "rank": 32, "mcr": 0.1, "iters": 2, "dtype": "f32"}}
+
+
+def _spec(cfg):
+    from powersgd_amd.workloads import CONFIGS
+    return CONFIGS[cfg] if cfg in CONFIGS else WIDE[cfg]
+
+
 def _port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -43,7 +55,7 @@ def _run(cfg, world, steps, port, env):
     from oracle import multiworker as MW
     from oracle import powersgd_oracle as O
     from powersgd_amd import Config, PowerSGD, _lib
-    from powersgd_amd.workloads import CONFIGS, hash_tensors
+    from powersgd_amd.workloads import hash_tensors
 
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -51,7 +63,7 @@ def _run(cfg, world, steps, port, env):
     try:
         stub = ctypes.CDLL(STUB)  # the same handle the library opened: one call counter
         stub.psgd_stub_calls.restype = ctypes.c_longlong
-        c = CONFIGS[cfg]
+        c = _spec(cfg)
         shapes = c["shapes"]
         dt = torch.bfloat16 if c["dtype"] == "bf16" else torch.float32
         psgd = PowerSGD([torch.zeros(s, device=dev, dtype=dt) for s in shapes],
@@ -93,7 +105,7 @@ def _run(cfg, world, steps, port, env):
 
 def _positive(_, port, cfg, world, steps):
     rep = _run(cfg, world, steps, port, {"PSGD_STUB_MODE": "sum"})
-    c_iters = {"cfg2_resnet50_r1": 2, "cfg3_resnet50_r4": 2, "cfg4_llama_r2_bf16": 1, "cfg5_lstm_r1_i4": 4}[cfg]
+    c_iters = _spec(cfg)["iters"]
     for t, (eo, er, calls, nunc) in enumerate(rep):
         bf16 = cfg.startswith("cfg4")
         tol = 4e-3 if bf16 else ((1e-5 if t == 0 else 1e-4))
@@ -104,7 +116,8 @@ def _positive(_, port, cfg, world, steps):
 
 
 @pytest.mark.parametrize("cfg,world", [("cfg2_resnet50_r1", 4), ("cfg3_resnet50_r4", 4),
-                                       ("cfg5_lstm_r1_i4", 8), ("cfg4_llama_r2_bf16", 2)])
+                                       ("cfg5_lstm_r1_i4", 8), ("cfg4_llama_r2_bf16", 2),
+                                       ("wide16", 2), ("wide32", 4)])
 def test_rccl_orchestration_world_w_vs_oracle(cfg, world):
     """psgd_aggregate_comm at world W, 2 steps, vs W reference workers."""
     torch.multiprocessing.spawn(_positive, args=(_port(), cfg, world, 2), nprocs=1, join=True)
