@@ -915,11 +915,8 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
     }
 }
 
-#ifndef PSGD_ODD_WPE
-#define PSGD_ODD_WPE 1
-#endif
 template <typename T, int RC, int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PSGD_ODD_WPE))) void k_odd_mfma(ProductArgs a) {
+__global__ __launch_bounds__(kBlock) void k_odd_mfma(ProductArgs a) {
     __shared__ __attribute__((aligned(16))) float xt[RC * 4 * kOddXT];
     __shared__ __attribute__((aligned(16))) float bs[(K > 0 ? K : 1) * kOddSW * 4 * RC];
     const Tile t = a.tiles[blockIdx.x];
