@@ -879,14 +879,55 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
         }
     };
 
-    issue(0);  // in flight while the strips are staged
-
     // Stage the strip's factor panels once per tile: xt[c][j] = X[j_begin + j][c]
     // (transposed: a lane's four B-operands of one k-step are one ds_read_b128) and
-    // bs[k][j][c] = B_k[j_begin + j][c] for the error-feedback correction.
+    // bs[k][j][c] = B_k[j_begin + j][c] for the error-feedback correction. This thread's X values
+    // (at most RP) are loaded BEFORE the tile's gradient loads, so that waiting for them (vmcnt
+    // counts in order) does not also wait for the gradient rows.
     {
         const gptr<const float> X = gconst<float>(a.x) + d.qoff + int64_t(j_begin) * r;
-        for (int idx = threadIdx.x; idx < sw * r; idx += kBlock) {
+        const int nx = sw * r;  // <= kOddSW * RP = kBlock * RP
+        // rank 32 and K >= 2: none (2 waves per SIMD would become 1). Rank 16, K = 1 (the
+        // I = 2 odd product): 83.5 -> 74.8 us (profiles/r06/wide/em9)
+        constexpr int NXP = (RP <= 16 && K <= 1) ? RP : 0;
+        float xs[NXP > 0 ? NXP : 1];
+#pragma unroll
+        for (int u = 0; u < NXP; ++u) {
+            const int idx = int(threadIdx.x) + u * kBlock;
+            xs[u] = X[idx < nx ? idx : 0];
+        }
+        // ... and the first error-feedback panel's (a term loaded after the gradient rows waits
+        // for them)
+        constexpr bool BP = K == 1 && NXP > 0;
+        float bp[BP ? NXP : 1];
+        if constexpr (BP) {
+            const gptr<const float> Bq = gconst<float>(a.res.q[0]) + d.qoff + int64_t(j_begin) * r;
+#pragma unroll
+            for (int u = 0; u < NXP; ++u) {
+                const int idx = int(threadIdx.x) + u * kBlock;
+                bp[u] = Bq[idx < nx ? idx : 0];
+            }
+        }
+        issue(0);  // in flight while the strips are staged
+        if constexpr (BP) {
+#pragma unroll
+            for (int u = 0; u < NXP; ++u) {
+                const int idx = int(threadIdx.x) + u * kBlock;
+                if (idx < nx) {
+                    const int j = idx / r, c = idx - j * r;
+                    bs[j * RP + c] = bp[u];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NXP; ++u) {
+            const int idx = int(threadIdx.x) + u * kBlock;
+            if (idx < nx) {
+                const int j = idx / r, c = idx - j * r;
+                xt[c * kOddXT + j] = xs[u];
+            }
+        }
+        for (int idx = int(threadIdx.x) + NXP * kBlock; idx < nx; idx += kBlock) {
             const int j = idx / r, c = idx - j * r;
             xt[c * kOddXT + j] = X[idx];
         }
@@ -897,7 +938,7 @@ __device__ __forceinline__ void odd_mfma_tile(const ProductArgs& a, const MatDes
         }
         if constexpr (K > 0) {
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
+            for (int k = BP ? 1 : 0; k < K; ++k) {
                 const gptr<const float> Bq = gconst<float>(a.res.q[k]) + d.qoff + int64_t(j_begin) * r;
                 for (int idx = threadIdx.x; idx < sw * r; idx += kBlock) {
                     const int j = idx / r, c = idx - j * r;
