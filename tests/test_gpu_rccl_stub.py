@@ -28,7 +28,8 @@ STUB = os.path.join(REPO, "tests", "stubs", "librccl_stub.so")
 # the all-reduced factors): ragged strips, a narrow matrix, an m % 4 != 0 matrix, a flat tail
 WIDE_SHAPES = [(300, 200), (64, 1000), (1000, 64), (96, 40), (333, 148), (200, 150), (40,), (130, 16, 3, 3)]
 WIDE = {"wide16": {"shapes": WIDE_SHAPES, "rank": 16, "mcr": 0.1, "iters": 2, "dtype": "f32"},
-        "wide32": {"shapes": WIDE_SHAPES, "rank": 32, "mcr": 0.1, "iters": 2, "dtype": "f32"}}
+        "wide32": {"shapes": WIDE_SHAPES, "rank": 32, "mcr": 0.1, "iters": 2, "dtype": "f32"},
+        "wide16bf": {"shapes": WIDE_SHAPES, "rank": 16, "mcr": 0.1, "iters": 2, "dtype": "bf16"}}
 
 
 def _spec(cfg):
@@ -107,17 +108,19 @@ def _positive(_, port, cfg, world, steps):
     rep = _run(cfg, world, steps, port, {"PSGD_STUB_MODE": "sum"})
     c_iters = _spec(cfg)["iters"]
     for t, (eo, er, calls, nunc) in enumerate(rep):
-        bf16 = cfg.startswith("cfg4")
+        bf16 = _spec(cfg)["dtype"] == "bf16"
         tol = 4e-3 if bf16 else ((1e-5 if t == 0 else 1e-4))
         check(eo, tol, cfg, world, t, "out")
         check(er, tol, cfg, world, t, "res")
-        # one collective per power iteration, plus the flat tail grouped with the last one
-        assert calls == c_iters + (1 if nunc else 0), (cfg, calls)
+        # one collective per power iteration, plus the flat tail grouped with the last one (fp32
+        # plans; a bf16 plan's uncompressed tensors are summed in their own dtype by the process
+        # group, powersgd.py, not through the library's fp32 collective)
+        assert calls == c_iters + (1 if nunc and not bf16 else 0), (cfg, calls)
 
 
 @pytest.mark.parametrize("cfg,world", [("cfg2_resnet50_r1", 4), ("cfg3_resnet50_r4", 4),
                                        ("cfg5_lstm_r1_i4", 8), ("cfg4_llama_r2_bf16", 2),
-                                       ("wide16", 2), ("wide32", 4)])
+                                       ("wide16", 2), ("wide32", 4), ("wide16bf", 2)])
 def test_rccl_orchestration_world_w_vs_oracle(cfg, world):
     """psgd_aggregate_comm at world W, 2 steps, vs W reference workers."""
     torch.multiprocessing.spawn(_positive, args=(_port(), cfg, world, 2), nprocs=1, join=True)
